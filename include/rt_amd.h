@@ -1,0 +1,221 @@
+/*
+ * rt_amd.h -- C-ABI drop-in boundary of the MI355X-native per-pixel ray tracer.
+ *
+ * Every entry point replaces one C++ seam of the reference renderer
+ * (catalinlup/RayTracer-Group27, paths relative to the reference root):
+ *
+ *   rt_create            BoundingVolumeHierarchy::BoundingVolumeHierarchy(Scene*)
+ *                        src/bounding_volume_hierarchy.h:24, .cpp:5-9 (+ scene upload)
+ *   rt_intersect         bool BoundingVolumeHierarchy::intersect(Ray&, HitInfo&, bool useBVH) const
+ *                        src/bounding_volume_hierarchy.h:33, .cpp:49-78
+ *   rt_shade             static glm::vec3 getFinalColor(Scene&, const BVH&, Ray, int level=0)
+ *                        src/main.cpp:129-301
+ *   rt_render            static void renderRayTracing(Scene&, const Trackball&, const BVH&, Screen&, ...)
+ *                        src/main.cpp:340-400 (+ Screen::setPixel src/screen.cpp:32-38)
+ *   rt_render_device     same as rt_render, band-partitioned, device-resident output (multi-GPU path)
+ *   rt_camera_from_trackball  Trackball::generateRay / position(), framework/src/trackball.cpp:65-98
+ *   rt_scene_load_obj    std::vector<Mesh> loadMesh(path, bool normalize), src/mesh.cpp:58-188
+ *   rt_scene_preset      Scene loadScene(SceneType, dataDir), src/scene.cpp:4-150
+ *   rt_destroy           ~BoundingVolumeHierarchy / scene teardown
+ *
+ * Conventions: plain pointers and sizes, no C++ or torch types.  Every function returns an
+ * int status: 0 = ok, < 0 = error (message via rt_last_error).  The caller owns every host
+ * buffer it passes; a context owns its device memory.  Calls on one context are synchronous
+ * and must not be made concurrently (the reference BVH is shared read-only by OpenMP threads;
+ * here the parallelism is inside the GPU launch).
+ */
+#ifndef RT_AMD_H
+#define RT_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+/* status codes */
+#define RT_OK 0
+#define RT_ERR_INVALID (-1)
+#define RT_ERR_IO (-2)
+#define RT_ERR_HIP (-3)
+#define RT_ERR_NOMEM (-4)
+#define RT_ERR_NO_DEVICE (-5)
+
+/* Material, src/mesh.h:23-33 (kd, ks{0}, shininess{1}, transparency{1}, optional<Image>). */
+typedef struct rt_material {
+    float kd[3];
+    float ks[3];
+    float shininess;
+    float transparency;
+    int has_texture; /* kdTexture.has_value(); textures are off in the render path (main.cpp:58) */
+    int pad_;
+} rt_material;
+
+/* Sphere, src/scene.h:48-53 */
+typedef struct rt_sphere {
+    float center[3];
+    float radius;
+    rt_material material;
+} rt_sphere;
+
+/* Light PODs, src/scene.h:55-83 */
+typedef struct rt_point_light { float position[3]; float color[3]; } rt_point_light;
+typedef struct rt_spherical_light { float position[3]; float radius; float color[3]; } rt_spherical_light;
+typedef struct rt_spot_light { float position[3]; float direction[3]; float angle; float color[3]; } rt_spot_light;
+typedef struct rt_plane_light { float position[3]; float width[3]; float height[3]; float color[3]; } rt_plane_light;
+
+/*
+ * Flat scene in scene order.  Triangles are listed mesh-major exactly as
+ * BoundingVolumeHierarchy::loadObjectsFromScene flattens them
+ * (src/bounding_volume_hierarchy.cpp:80-99): for each mesh, for each of its triangles,
+ * the three Vertex records {p, n, texCoord} (src/mesh.h:16-21).
+ */
+typedef struct rt_scene_desc {
+    int num_triangles;
+    const float* positions;   /* [num_triangles][3 corners][3] */
+    const float* normals;     /* [num_triangles][3 corners][3] */
+    const float* texcoords;   /* [num_triangles][3 corners][2] or NULL (zeros) */
+    const int* mesh_index;    /* [num_triangles] index into materials (== triangle_materials) */
+    int num_meshes;
+    const rt_material* materials; /* [num_meshes] */
+    int num_spheres;
+    const rt_sphere* spheres;
+    int num_point_lights;
+    const rt_point_light* point_lights;
+    int num_spherical_lights;
+    const rt_spherical_light* spherical_lights;
+    int num_spot_lights;
+    const rt_spot_light* spot_lights;
+    int num_plane_lights;
+    const rt_plane_light* plane_lights;
+} rt_scene_desc;
+
+/*
+ * Camera constants, computed once per frame on the host with the reference Trackball math
+ * (framework/src/trackball.cpp:65-68,87-98): ray.origin = position,
+ * ray.direction = quat * normalize(vec3(-ndc.x*half_width, ndc.y*half_height, 1)).
+ */
+typedef struct rt_camera {
+    float position[3];
+    float quat[4];      /* x, y, z, w  (glm::quat(eulerAngles)) */
+    float half_height;  /* tan(fovy/2) */
+    float half_width;   /* aspect * half_height */
+} rt_camera;
+
+/* Render knobs: the reference's globals, src/main.cpp:54-64,123-127 (defaults in brackets). */
+typedef struct rt_params {
+    int max_reflection_level;     /* [5] */
+    int sphere_light_ray_count;   /* [10] */
+    int plane_light_1D_ray_count; /* [3] */
+    int glossy_ray_count;         /* [10]; parity configs use 1 (no rand()) */
+    float refraction_factor;      /* [0.8] */
+    int use_bvh;                  /* [0] useBVH for primary/secondary rays; shadow rays always use the BVH */
+    int anti_aliasing;            /* renderRayTracing(..., anti_aliasing) */
+    int multiple_rays;            /* renderRayTracing(..., multipleRays, sampleSize) */
+    int sample_size;              /* [4]: 4, 16 or 64 */
+    int barycentric_mode;         /* 0 = "unthresholded" (defined semantics for the reference's UB) */
+    uint64_t rng_seed;            /* glossy_ray_count > 1: Philox-4x32 stream seed (replaces rand()) */
+} rt_params;
+
+/* Ray, framework/include/ray.h:11-15 (origin, direction, t{FLT_MAX}) */
+typedef struct rt_ray {
+    float origin[3];
+    float direction[3];
+    float t; /* initial ray.t (FLT_MAX for a fresh Ray) */
+} rt_ray;
+
+/* HitInfo subset, src/ray_tracing.h:6-37 */
+typedef struct rt_hit {
+    int hit;              /* return value of intersect() */
+    float t;              /* ray.t after the call */
+    float normal[3];      /* hitInfo.normal (interpolated, not normalized, for triangles) */
+    float hit_point[3];   /* hitInfo.hitPoint */
+    float uv[2];          /* hitInfo.texCoord */
+    int material_index;   /* mesh index (triangles) / -1 (spheres) */
+    int prim_id;          /* scene-order triangle index, or num_triangles + sphere index */
+    int is_triangle;
+} rt_hit;
+
+/* Per-launch counters (rt_render_device / rt_render). */
+typedef struct rt_stats {
+    uint64_t rays;          /* intersect() calls: primary + secondary + shadow segments */
+    uint64_t node_visits;   /* BVH2 nodes fetched (counting builds only, else 0) */
+    uint64_t tri_tests;     /* triangle records fetched (counting builds only, else 0) */
+    uint64_t hits;          /* closest hits shaded (counting builds only, else 0) */
+    float kernel_ms;        /* device time of the render launch(es), HIP events */
+    float pad_;
+} rt_stats;
+
+typedef struct rt_ctx rt_ctx;
+typedef struct rt_scene rt_scene;
+
+int rt_abi_version(void);
+int rt_last_error(char* buf, size_t len);
+
+/* ---- scene ingest (host) ---- */
+/* loadMesh (src/mesh.cpp:58-188) with Assimp 5.0.1 OBJ semantics; appends the meshes to scene. */
+int rt_scene_new(rt_scene** out);
+int rt_scene_load_obj(rt_scene* scene, const char* path, int normalize, int shininess_x4);
+/* loadScene presets (src/scene.cpp:4-150).  preset: SceneType enum value (src/scene.h:14-34). */
+int rt_scene_preset(rt_scene* scene, int preset, const char* data_dir, int shininess_x4);
+int rt_scene_add_sphere(rt_scene* scene, const rt_sphere* s);
+int rt_scene_add_point_light(rt_scene* scene, const rt_point_light* l);
+int rt_scene_add_spherical_light(rt_scene* scene, const rt_spherical_light* l);
+int rt_scene_add_spot_light(rt_scene* scene, const rt_spot_light* l);
+int rt_scene_add_plane_light(rt_scene* scene, const rt_plane_light* l);
+int rt_scene_clear_lights(rt_scene* scene);
+int rt_scene_set_material(rt_scene* scene, int mesh, const rt_material* m);
+/* Flat view (pointers stay valid until the scene is modified or freed). */
+int rt_scene_desc_get(const rt_scene* scene, rt_scene_desc* out);
+int rt_scene_free(rt_scene* scene);
+/* Deterministic 800k-triangle (2,3) torus-knot stand-in for the missing data/dragon.obj. */
+int rt_write_dragon_proxy(const char* obj_path, int u_segments, int v_segments);
+
+/* ---- camera ---- */
+int rt_camera_from_trackball(const float look_at[3], const float euler_radians[3], float distance,
+                             float fovy_radians, float aspect, rt_camera* out);
+
+/* ---- device context ---- */
+int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out);
+int rt_destroy(rt_ctx* ctx);
+
+/* Whole frame to host memory: rgb_out = W*H*3 floats in Screen::m_textureData order. */
+int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_params* params, int width, int height,
+              float* rgb_out, rt_stats* stats);
+
+/*
+ * Band-partitioned render into DEVICE memory on a caller stream (hipStream_t or NULL).
+ * The image is cut into bands of band_rows rows (from y = 0); this call renders the bands
+ * b with b % band_count == band_rank and writes them densely, band after band, into
+ * d_rgb_out ([n_local_bands][band_rows][width][3] floats, row r of a band = image row y in
+ * reference y order, i.e. before the setPixel flip).  The host gathers and un-permutes.
+ */
+int rt_render_device(rt_ctx* ctx, const rt_camera* cam, const rt_params* params, int width,
+                     int height, int band_rows, int band_rank, int band_count, float* d_rgb_out,
+                     void* stream, rt_stats* stats);
+/* Un-permute gathered band buffers ([band_count][max_local_bands][band_rows][W][3]) into the
+ * setPixel layout on the device. */
+int rt_unpermute_bands_device(int width, int height, int band_rows, int band_count,
+                              const float* d_gathered, float* d_image, void* stream);
+
+/* Per-ray entry points used by the facade and the parity tests (host buffers). */
+int rt_intersect(rt_ctx* ctx, const rt_ray* rays, int n, int use_bvh, rt_hit* hits);
+int rt_shade(rt_ctx* ctx, const rt_ray* rays, int n, const rt_params* params, float* rgb,
+             uint64_t* rays_per_sample);
+
+/* Counting build of the same kernel (node visits, triangle records, hits) for roofline accounting. */
+int rt_set_counting(int on);
+
+/* Introspection for tests / roofline accounting. */
+int rt_ctx_info(rt_ctx* ctx, int* num_nodes, int* num_tri_records, int* ref_bvh_nodes,
+                int* ref_bvh_levels);
+/* Device math self-test: out[i] = {sqrtf(x), 1/x, x/y, powf(x,y)} bits for parity of the math lib. */
+int rt_selftest_math(rt_ctx* ctx, const float* x, const float* y, int n, float* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_AMD_H */

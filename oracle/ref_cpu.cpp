@@ -1,0 +1,813 @@
+// ORACLE -- test infrastructure, not product code.
+//
+// CPU restatement of the reference hot path of catalinlup/RayTracer-Group27 (paths relative to
+// the reference root).  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
+// may load this library, and only as the checker / the timed CPU baseline; the product path
+// (raytracer-group27_amd/librt_amd.so) never links or calls it.
+//
+// It is written independently of the HIP product (own vector type, own BVH, recursion
+// instead of an explicit stack) and follows the reference call structure:
+//   renderRayTracing            src/main.cpp:340-400 (pixel loop, AA, getPixelRays :309-335)
+//   Trackball::generateRay      framework/src/trackball.cpp:65-68, 87-98
+//   getFinalColor / calcColor   src/main.cpp:112-301
+//   BVH::intersect              src/bounding_volume_hierarchy.cpp:49-78 (brute force)
+//   BVH build + intersectBVH    src/bounding_volume_hierarchy.cpp:80-448 (max_level 4, h:67)
+//   primitive tests             src/ray_tracing.cpp:15-316
+//   cansee + light gathering    src/shadow.cpp:32-321
+// Arithmetic follows glm 0.9.9.8's non-SIMD op order (dot = (x+y)+z, normalize = v*(1/sqrt),
+// min/max as ternaries) and C++ promotions (std::pow(float,int) -> double).
+//
+// PARITY STATUS: parity unpinned.  The reference ships no tests, golden vectors or fixtures
+// for this path, and it cannot be built here without stand-ins for glm,
+// gsl-lite, Assimp, GLFW and ImGui, which the task forbids; render.bmp has an unrecorded camera.
+// Where the reference is undefined (uninitialised barycentrics when barycentricCoordinates
+// returns false, src/ray_tracing.cpp:147-157) this restatement uses the "unthresholded"
+// definition, shared with the GPU path.
+#include <cfloat>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+#include <algorithm>
+#include <array>
+#include <queue>
+#include <utility>
+
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#include "../include/rt_amd.h"
+
+namespace oracle {
+
+struct V3 {
+    float x = 0, y = 0, z = 0;
+    V3() = default;
+    V3(float a, float b, float c) : x(a), y(b), z(c) {}
+    explicit V3(float s) : x(s), y(s), z(s) {}
+    static V3 of(const float* p) { return V3(p[0], p[1], p[2]); }
+};
+static inline V3 operator+(const V3& a, const V3& b) { return V3(a.x + b.x, a.y + b.y, a.z + b.z); }
+static inline V3 operator-(const V3& a, const V3& b) { return V3(a.x - b.x, a.y - b.y, a.z - b.z); }
+static inline V3 operator-(const V3& a) { return V3(-a.x, -a.y, -a.z); }
+static inline V3 operator*(const V3& a, const V3& b) { return V3(a.x * b.x, a.y * b.y, a.z * b.z); }
+static inline V3 operator*(const V3& a, float s) { return V3(a.x * s, a.y * s, a.z * s); }
+static inline V3 operator*(float s, const V3& a) { return V3(s * a.x, s * a.y, s * a.z); }
+static inline V3 operator/(const V3& a, float s) { return V3(a.x / s, a.y / s, a.z / s); }
+static inline V3& operator+=(V3& a, const V3& b) { return a = a + b; }
+static inline float vdot(const V3& a, const V3& b) {
+    V3 m = a * b;
+    return m.x + m.y + m.z;
+}
+static inline V3 vcross(const V3& a, const V3& b) {
+    return V3(a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y);
+}
+static inline float vlength(const V3& v) { return std::sqrt(vdot(v, v)); }
+static inline V3 vnormalize(const V3& v) { return v * (1.0f / std::sqrt(vdot(v, v))); }
+static inline V3 vreflect(const V3& i, const V3& n) { return i - n * vdot(n, i) * 2.0f; }
+static inline float fmin_g(float a, float b) { return (b < a) ? b : a; }  // glm::min / std::min
+static inline float fmax_g(float a, float b) { return (a < b) ? b : a; }  // glm::max / std::max
+
+struct Mat {
+    V3 kd, ks;
+    float shininess = 1.0f;
+    float transparency = 1.0f;
+};
+struct Vert {
+    V3 p, n;
+    float u = 0, v = 0;
+};
+struct Sph {
+    V3 center;
+    float radius = 1.0f;
+    Mat mat;
+};
+struct Ray {
+    V3 origin;
+    V3 direction{0.0f, 0.0f, -1.0f};
+    float t = FLT_MAX;
+};
+struct Hit {
+    V3 normal, hitPoint;
+    int material_index = 0;
+    Mat sphere_material;
+    float u = 0, v = 0;
+    bool is_triangle = false;
+    int prim = -1;
+    Mat& material(std::vector<Mat>& mats) { return is_triangle ? mats[material_index] : sphere_material; }
+};
+struct Light {  // what getPointLights & co. return (src/shadow.h:14-20)
+    V3 color;
+    float intensity, cosL, cosS;
+};
+
+struct Node {
+    bool leaf = false;
+    std::vector<int> kids;
+    std::vector<char> tri;
+    V3 lo, hi;
+};
+
+struct Scene {
+    std::vector<std::array<Vert, 3>> tris;
+    std::vector<int> tri_mesh;
+    std::vector<Mat> mats;
+    std::vector<Sph> spheres;
+    std::vector<rt_point_light> pls;
+    std::vector<rt_spherical_light> sls;
+    std::vector<rt_spot_light> spots;
+    std::vector<rt_plane_light> planes;
+    std::vector<Node> nodes;
+};
+
+// ---------------------------------------------------------------- primitives (ray_tracing.cpp)
+// isZero/isEqual (src/ray_tracing.cpp:15-24) only gate barycentricCoordinates' return value,
+// which the "unthresholded" definition below does not consult.
+
+static bool point_in_triangle(const V3& a, const V3& b, const V3& c, const V3& n, const V3& p) {
+    const bool e0 = vdot(vcross(p - a, c - a), n) >= 0;
+    const bool e1 = vdot(vcross(p - c, b - c), n) >= 0;
+    const bool e2 = vdot(vcross(p - b, a - b), n) >= 0;
+    return (e0 && e1 && e2) || (!e0 && !e1 && !e2);
+}
+
+static void plane_of(const V3& a, const V3& b, const V3& c, V3& n, float& D) {
+    n = vnormalize(vcross(a - c, b - c));
+    D = vdot(n, a);
+}
+
+static bool hit_plane(const V3& n, float D, Ray& r) {
+    const float nd = vdot(vnormalize(r.direction), n);
+    if (nd == 0) return false;
+    const float t = (D - vdot(r.origin, n)) / nd;
+    if (!(t >= 0)) return false;
+    if (!(t < r.t)) return false;
+    r.t = t;
+    return true;
+}
+
+static bool hit_triangle_flat(const V3& a, const V3& b, const V3& c, Ray& r, Hit& h, int mat) {
+    const float keep = r.t;
+    V3 n;
+    float D;
+    plane_of(a, b, c, n, D);
+    if (!hit_plane(n, D, r)) return false;
+    const V3 p = r.origin + r.direction * r.t;
+    if (!point_in_triangle(a, b, c, n, p)) {
+        r.t = keep;
+        return false;
+    }
+    h.normal = n;
+    h.hitPoint = p;
+    h.material_index = mat;
+    return true;
+}
+
+static float par_area(const V3& a, const V3& b, const V3& c) { return vlength(vcross(b - a, c - a)); }
+
+// barycentricCoordinates with the "unthresholded" definition: the thresholds only decide
+// whether the reference's result is defined; the coordinates are the same formula either way.
+static V3 barycentric(const V3& a, const V3& b, const V3& c, const V3& p) {
+    const float A = par_area(a, b, c);
+    if (!(A > 0.0f)) return V3(0.0f);
+    return V3(par_area(p, b, c) / A, par_area(a, p, c) / A, par_area(a, b, p) / A);
+}
+
+static bool hit_triangle(const Vert& a, const Vert& b, const Vert& c, Ray& r, Hit& h, int mat, int prim) {
+    const float before = r.t;
+    if (!hit_triangle_flat(a.p, b.p, c.p, r, h, mat)) return false;
+    if (r.t < before) {
+        h.is_triangle = true;
+        h.prim = prim;
+    }
+    const V3 bc = barycentric(a.p, b.p, c.p, h.hitPoint);
+    const V3 face = h.normal;
+    h.normal = a.n * bc.x + b.n * bc.y + c.n * bc.z;
+    if (vdot(h.normal, face) < 0) h.normal = -h.normal;
+    h.u = a.u * bc.x + b.u * bc.y + c.u * bc.z;
+    h.v = a.v * bc.x + b.v * bc.y + c.v * bc.z;
+    return true;
+}
+
+static bool hit_sphere(const Sph& s, Ray& r, Hit& h, int prim) {
+    const V3 m = r.origin - s.center;
+    const V3& d = r.direction;
+    // glm::pow(float, int) == std::pow(double, double): computed in double, stored as float
+    const float A = std::pow((double)d.x, 2) + std::pow((double)d.y, 2) + std::pow((double)d.z, 2);
+    const float B = 2 * (d.x * m.x + d.y * m.y + d.z * m.z);
+    const float C = std::pow((double)m.x, 2) + std::pow((double)m.y, 2) + std::pow((double)m.z, 2) -
+                    std::pow((double)s.radius, 2);
+    const float disc = std::pow((double)B, 2) - 4 * A * C;
+    if (!(disc >= 0)) return false;
+    float t0 = (-B + std::sqrt(disc)) / (2 * A);
+    float t1 = (-B - std::sqrt(disc)) / (2 * A);
+    if (t0 < 0) t0 = t1;
+    if (t1 < 0) t1 = t0;
+    const float tm = fmin_g(t0, t1);
+    if (!(tm > 0 && tm < r.t)) return false;
+    r.t = tm;
+    h.hitPoint = r.origin + r.t * r.direction;
+    h.normal = vnormalize(h.hitPoint - s.center);
+    h.sphere_material = s.mat;
+    h.is_triangle = false;
+    h.prim = prim;
+    return true;
+}
+
+static bool hit_box(const V3& lo, const V3& hi, Ray& r) {
+    if (lo.x == FLT_MAX && lo.y == FLT_MAX && lo.z == FLT_MAX && hi.x == -FLT_MAX && hi.y == -FLT_MAX &&
+        hi.z == -FLT_MAX)
+        return false;
+    const V3 d = vnormalize(r.direction);
+    const float ax = (lo.x - r.origin.x) / d.x, bx = (hi.x - r.origin.x) / d.x;
+    const float ay = (lo.y - r.origin.y) / d.y, by = (hi.y - r.origin.y) / d.y;
+    const float az = (lo.z - r.origin.z) / d.z, bz = (hi.z - r.origin.z) / d.z;
+    if (r.origin.x > lo.x && r.origin.y > lo.y && r.origin.z > lo.z && r.origin.x < hi.x && r.origin.y < hi.y &&
+        r.origin.z < hi.z) {
+        float best = FLT_MAX;
+        for (float v : {ax, bx, ay, by, az, bz})
+            if (v > 0 && v < best) best = v;
+        r.t = best;
+        return true;
+    }
+    const float tin = fmax_g(fmax_g(fmin_g(ax, bx), fmin_g(ay, by)), fmin_g(az, bz));
+    const float tout = fmin_g(fmin_g(fmax_g(ax, bx), fmax_g(ay, by)), fmax_g(az, bz));
+    if (tin > tout || tout < 0) return false;
+    r.t = tin;
+    return true;
+}
+
+// ---------------------------------------------------------------- BVH (bounding_volume_hierarchy.cpp)
+static void node_bounds(const Scene& sc, const std::vector<int>& ids, const std::vector<char>& tri, V3& lo, V3& hi) {
+    lo = V3(FLT_MAX);
+    hi = V3(-FLT_MAX);
+    auto vmin = [](const V3& a, const V3& b) { return V3(fmin_g(a.x, b.x), fmin_g(a.y, b.y), fmin_g(a.z, b.z)); };
+    auto vmax = [](const V3& a, const V3& b) { return V3(fmax_g(a.x, b.x), fmax_g(a.y, b.y), fmax_g(a.z, b.z)); };
+    for (size_t i = 0; i < ids.size(); ++i) {
+        if (tri[i]) {
+            const auto& t = sc.tris[ids[i]];
+            lo = vmin(vmin(lo, t[0].p), vmin(t[1].p, t[2].p));
+            hi = vmax(vmax(hi, t[0].p), vmax(t[1].p, t[2].p));
+        } else {
+            const Sph& s = sc.spheres[ids[i]];
+            const V3 a = s.center - V3(s.radius), b = s.center + V3(s.radius);
+            lo = vmin(lo, vmin(a, b));
+            hi = vmax(hi, vmax(a, b));
+        }
+    }
+}
+
+static float split_key(const Scene& sc, int id, bool tri, int level) {
+    const int axis = level % 3;
+    if (tri) {
+        const auto& t = sc.tris[id];
+        if (axis == 0) return (t[0].p.x + t[1].p.x + t[2].p.x) / 3;
+        if (axis == 1) return (t[0].p.y + t[1].p.y + t[2].p.y) / 3;
+        return (t[0].p.z + t[1].p.z + t[2].p.z) / 3;
+    }
+    const V3& c = sc.spheres[id].center;
+    return axis == 0 ? c.x : (axis == 1 ? c.y : c.z);
+}
+
+static void build_bvh(Scene& sc) {
+    const int max_level = 4;
+    std::vector<std::vector<int>> ids;
+    std::vector<std::vector<char>> kinds;
+    auto make = [&](std::vector<int> i, std::vector<char> k, int level) {
+        Node n;
+        n.leaf = i.size() <= 1 || level >= max_level;
+        node_bounds(sc, i, k, n.lo, n.hi);
+        sc.nodes.push_back(n);
+        ids.push_back(std::move(i));
+        kinds.push_back(std::move(k));
+        return (int)sc.nodes.size() - 1;
+    };
+    std::vector<int> all;
+    std::vector<char> allk;
+    for (size_t i = 0; i < sc.tris.size(); ++i) {
+        all.push_back((int)i);
+        allk.push_back(1);
+    }
+    for (size_t i = 0; i < sc.spheres.size(); ++i) {
+        all.push_back((int)i);
+        allk.push_back(0);
+    }
+    std::queue<std::pair<int, int>> work;
+    work.push({make(all, allk, 0), 0});
+    while (!work.empty()) {
+        auto [ni, level] = work.front();
+        work.pop();
+        std::vector<int> cur = ids[ni];
+        std::vector<char> curk = kinds[ni];
+        if (sc.nodes[ni].leaf) {
+            sc.nodes[ni].kids = cur;
+            sc.nodes[ni].tri = curk;
+            continue;
+        }
+        ++level;
+        std::vector<std::pair<float, int>> keyed;
+        for (size_t i = 0; i < cur.size(); ++i) keyed.emplace_back(split_key(sc, cur[i], curk[i] != 0, level), (int)i);
+        std::sort(keyed.begin(), keyed.end());
+        std::vector<int> li, ri;
+        std::vector<char> lk, rk;
+        const size_t nl = (cur.size() + 1) / 2;
+        for (size_t i = 0; i < keyed.size(); ++i) {
+            const int src = keyed[i].second;
+            if (i < nl) {
+                li.push_back(cur[src]);
+                lk.push_back(curk[src]);
+            } else {
+                ri.push_back(cur[src]);
+                rk.push_back(curk[src]);
+            }
+        }
+        if (!li.empty()) {
+            const int c = make(li, lk, level);
+            work.push({c, level});
+            sc.nodes[ni].kids.push_back(c);
+        }
+        if (!ri.empty()) {
+            const int c = make(ri, rk, level);
+            work.push({c, level});
+            sc.nodes[ni].kids.push_back(c);
+        }
+    }
+}
+
+static bool walk_bvh(const Scene& sc, int ni, Ray& r, Hit& h) {
+    const float keep = r.t;
+    const bool in = hit_box(sc.nodes[ni].lo, sc.nodes[ni].hi, r);
+    r.t = keep;
+    if (!in) return false;
+    const Node& n = sc.nodes[ni];
+    bool any = false;
+    if (n.leaf) {
+        for (size_t i = 0; i < n.kids.size(); ++i) {
+            const int id = n.kids[i];
+            if (n.tri[i]) {
+                const auto& t = sc.tris[id];
+                any |= hit_triangle(t[0], t[1], t[2], r, h, sc.tri_mesh[id], id);
+            } else {
+                any |= hit_sphere(sc.spheres[id], r, h, (int)sc.tris.size() + id);
+            }
+        }
+        return any;
+    }
+    for (int c : n.kids) any |= walk_bvh(sc, c, r, h);
+    return any;
+}
+
+struct Counter {
+    uint64_t rays = 0;
+};
+
+static bool intersect(const Scene& sc, Ray& r, Hit& h, bool use_bvh, Counter& cnt) {
+    cnt.rays++;
+    if (!use_bvh) {
+        bool any = false;
+        for (size_t i = 0; i < sc.tris.size(); ++i) {
+            const auto& t = sc.tris[i];
+            if (hit_triangle(t[0], t[1], t[2], r, h, sc.tri_mesh[i], (int)i)) any = true;
+        }
+        for (size_t s = 0; s < sc.spheres.size(); ++s) any |= hit_sphere(sc.spheres[s], r, h, (int)(sc.tris.size() + s));
+        return any;
+    }
+    if (sc.nodes.empty()) return false;
+    return walk_bvh(sc, 0, r, h);
+}
+
+// ---------------------------------------------------------------- lights (shadow.cpp)
+static bool cansee(Scene& sc, const V3& from, const V3& to, float& intensity, Counter& cnt) {
+    V3 d = to - from;
+    float dist = vlength(d);
+    d = vnormalize(d);
+    Ray r;
+    r.origin = from + 0.0005f * d;
+    r.direction = d;
+    Hit h;
+    while (dist > 0.0005f) {
+        const bool hit = intersect(sc, r, h, true, cnt);
+        Mat& m = h.material(sc.mats);
+        if (!hit || r.t > dist - 2 * 0.0005f) return true;
+        if (m.transparency != 1.0f) {
+            dist -= r.t;
+            r.t = FLT_MAX;
+            r.origin = h.hitPoint + 0.0005f * r.direction;
+            const float c = std::abs(vdot(r.direction, h.normal));
+            const float R0 = m.transparency;
+            intensity *= 1 - (R0 + (1 - R0) * std::pow((double)(1 - c), 5.0));
+        } else {
+            return false;
+        }
+    }
+    return true;
+}
+
+struct Rot {  // glm::mat3 column-major m[col][row]
+    float m[3][3];
+};
+static Rot rodrigues(float angle, const V3& ax) {
+    Rot C{{{0, ax.z, -ax.y}, {-ax.z, 0, ax.x}, {ax.y, -ax.x, 0}}};
+    Rot CC;
+    for (int c = 0; c < 3; ++c)
+        for (int w = 0; w < 3; ++w) CC.m[c][w] = C.m[0][w] * C.m[c][0] + C.m[1][w] * C.m[c][1] + C.m[2][w] * C.m[c][2];
+    const float s = std::sin(angle), omc = 1 - std::cos(angle);
+    Rot R;
+    for (int c = 0; c < 3; ++c)
+        for (int w = 0; w < 3; ++w) R.m[c][w] = ((c == w ? 1.0f : 0.0f) + C.m[c][w] * s) + CC.m[c][w] * omc;
+    return R;
+}
+static V3 rot_apply(const Rot& R, const V3& v) {
+    return V3(R.m[0][0] * v.x + R.m[1][0] * v.y + R.m[2][0] * v.z, R.m[0][1] * v.x + R.m[1][1] * v.y + R.m[2][1] * v.z,
+              R.m[0][2] * v.x + R.m[1][2] * v.y + R.m[2][2] * v.z);
+}
+
+static Light make_light(const V3& color, float intensity, const Hit& h, const V3& refl, const V3& lpos) {
+    Light l;
+    l.color = color;
+    l.intensity = intensity;
+    l.cosL = std::abs(vdot(vnormalize(h.normal), vnormalize(lpos - h.hitPoint)));
+    l.cosS = fmax_g(0.0f, vdot(vnormalize(refl), vnormalize(lpos - h.hitPoint)));
+    return l;
+}
+
+static void gather_lights(Scene& sc, const Hit& h, const V3& refl, const rt_params& P, std::vector<Light>& out,
+                          Counter& cnt) {
+    for (const auto& L : sc.pls) {
+        float I = 1.0f;
+        if (cansee(sc, h.hitPoint, V3::of(L.position), I, cnt))
+            out.push_back(make_light(V3::of(L.color), I, h, refl, V3::of(L.position)));
+    }
+    for (const auto& L : sc.sls) {
+        const V3 pos = V3::of(L.position);
+        float I = 1.0f, sum = 1.0f;
+        int seen = 0;
+        if (cansee(sc, h.hitPoint, pos, sum, cnt)) seen++;
+        V3 d = vnormalize(pos - h.hitPoint);
+        V3 other = d;
+        if (d.x != 0) {
+            other.y = -d.x;
+            other.x = d.y;
+        } else {
+            other.y = -d.z;
+            other.z = d.y;
+        }
+        V3 perp = vnormalize(vcross(d, other)) * L.radius;
+        int count = P.sphere_light_ray_count;
+        const int rings = std::max(1, (int)(count / std::round(std::sqrt(2 * 3.14159365358979f * count))));
+        const int spokes = (count - 1) / rings;
+        count = rings * spokes + 1;
+        const Rot R = rodrigues(2 * 3.14159365358979f / spokes, d);
+        for (int i = 0; i < spokes; i++) {
+            for (int j = 0; j < rings; j++) {
+                I = 1.0f;
+                if (cansee(sc, h.hitPoint, pos + ((rings - j) / (float)rings) * perp, I, cnt)) {
+                    seen++;
+                    sum += I;
+                }
+            }
+            perp = rot_apply(R, perp);
+        }
+        if (seen > 0) out.push_back(make_light(V3::of(L.color), sum / (float)count, h, refl, pos));
+    }
+    for (const auto& L : sc.spots) {
+        const V3 pos = V3::of(L.position);
+        if (vdot(vnormalize(V3::of(L.direction)), vnormalize(h.hitPoint - pos)) >
+            std::cos(L.angle * static_cast<float>(0.01745329251994329576923690768489))) {
+            float I = 1.0f;
+            if (cansee(sc, h.hitPoint, pos, I, cnt)) out.push_back(make_light(V3::of(L.color), I, h, refl, pos));
+        }
+    }
+    for (const auto& L : sc.planes) {
+        const int k = P.plane_light_1D_ray_count;
+        float acc = 0;
+        int nh = 0;
+        float best_cos = 0, sumI = 0, I = 1;
+        const V3 w = V3::of(L.width), hh = V3::of(L.height), pos = V3::of(L.position);
+        const V3 step_x = (1.0f / (k - 1)) * w, step_y = (1.0f / (k - 1)) * hh;
+        V3 row = pos;
+        const V3 n = vnormalize(vcross(w, hh));
+        if (vdot(vnormalize(h.hitPoint - (pos + 0.5f * (w + hh))), n) > 0) {
+            for (int i = 0; i < k; i++) {
+                V3 q = row;
+                for (int j = 0; j < k; j++) {
+                    I = 1;
+                    if (cansee(sc, h.hitPoint, q, I, cnt)) {
+                        sumI += I;
+                        acc += fmax_g(vdot(vnormalize(h.hitPoint - q), n), 0.0f) / vlength(h.hitPoint - q);
+                        nh++;
+                        best_cos = fmax_g(best_cos, vdot(vnormalize(refl), vnormalize(q - h.hitPoint)));
+                    }
+                    q += step_x;
+                }
+                row += step_y;
+            }
+        }
+        if (acc > 0) {
+            Light l;
+            l.color = V3::of(L.color);
+            l.intensity = (sumI / nh) * acc / (float)(k * k);
+            l.cosL = 1;
+            l.cosS = best_cos;
+            out.push_back(l);
+        }
+    }
+}
+
+static V3 phong(const Light& l, const Mat& m) {
+    const V3 diffuse = m.kd * l.color * l.intensity * l.cosL;
+    V3 spec(0.0f);
+    if (m.shininess > 0) spec = l.color * m.ks * std::pow(l.cosS, m.shininess);
+    return diffuse + spec;
+}
+
+// ---------------------------------------------------------------- getFinalColor (main.cpp:129-301)
+static V3 final_color(Scene& sc, const rt_params& P, Ray ray, int level, Counter& cnt) {
+    Hit h;
+    if (!intersect(sc, ray, h, P.use_bvh != 0, cnt)) return V3(0.0f);
+    V3 color(0.0f);
+    const V3 refl = vreflect(vnormalize(ray.direction), vnormalize(h.normal));
+    const Mat m = h.material(sc.mats);
+    std::vector<Light> lights;
+    gather_lights(sc, h, refl, P, lights, cnt);
+    for (const Light& l : lights) color += phong(l, m);
+    if (level >= P.max_reflection_level) return color;
+    if (m.transparency == 1.0f) {
+        if (m.ks.x > 0 || m.ks.y > 0 || m.ks.z > 0) {
+            V3 mirror(0.0f);
+            Ray rr;
+            rr.origin = h.hitPoint + 0.01f * refl;
+            rr.direction = refl;
+            mirror += m.ks * final_color(sc, P, rr, level + 1, cnt);
+            if (m.shininess != 0) {
+                // glossy_ray_count > 1 draws rand() here (main.cpp:227-249); not restated.
+                color += m.ks * mirror / (float)P.glossy_ray_count;
+            } else {
+                color += m.ks * mirror;
+            }
+        }
+    } else {
+        const V3 l = vnormalize(ray.direction);
+        const V3 n = vnormalize(h.normal);
+        const float r = P.refraction_factor;
+        const float c = std::abs(vdot(l, n));
+        V3 refr = r * l + (r * c - std::sqrt(1 - r * r * (1 - c * c))) * n;
+        refr = vnormalize(refr);
+        const float R0 = m.transparency;
+        const float reflect_part = R0 + (1 - R0) * std::pow((double)(1 - c), 5.0);
+        const float refract_part = 1 - reflect_part;
+        Ray a;
+        a.origin = h.hitPoint + 0.01f * refl;
+        a.direction = refl;
+        color += reflect_part * final_color(sc, P, a, level + 1, cnt);
+        if (r * r * (1 - c * c) <= 1.0f) {
+            Ray b;
+            b.origin = h.hitPoint + 0.01f * refr;
+            b.direction = refr;
+            color += refract_part * final_color(sc, P, b, level + 1, cnt);
+        }
+    }
+    return color;
+}
+
+// ---------------------------------------------------------------- camera (trackball.cpp)
+struct Cam {
+    V3 pos;
+    float qx, qy, qz, qw;
+    float hh, hw;
+};
+static V3 qrot(const Cam& c, const V3& v) {
+    const V3 q(c.qx, c.qy, c.qz);
+    const V3 uv = vcross(q, v);
+    const V3 uuv = vcross(q, uv);
+    return v + ((uv * c.qw) + uuv) * 2.0f;
+}
+static Cam make_cam(const float look[3], const float e[3], float dist, float fovy, float aspect) {
+    Cam c;
+    const V3 half = V3(e[0], e[1], e[2]) * 0.5f;
+    const float cx = std::cos(half.x), cy = std::cos(half.y), cz = std::cos(half.z);
+    const float sx = std::sin(half.x), sy = std::sin(half.y), sz = std::sin(half.z);
+    c.qw = cx * cy * cz + sx * sy * sz;
+    c.qx = sx * cy * cz - cx * sy * sz;
+    c.qy = cx * sy * cz + sx * cy * sz;
+    c.qz = cx * cy * sz - sx * sy * cz;
+    c.pos = V3(look[0], look[1], look[2]) + qrot(c, V3(0, 0, -dist));
+    c.hh = std::tan(fovy / 2.0f);
+    c.hw = aspect * c.hh;
+    return c;
+}
+static Ray camera_ray(const Cam& c, float px, float py) {
+    const V3 local = vnormalize(V3(-px * c.hw, py * c.hh, 1.0f));
+    Ray r;
+    r.origin = c.pos;
+    r.direction = qrot(c, local);
+    r.t = FLT_MAX;
+    return r;
+}
+
+static V3 render_pixel(Scene& sc, const Cam& cam, const rt_params& P, int W, int H, int x, int y, Counter& cnt) {
+    const float nx = float(x) / W * 2.0f - 1.0f;
+    const float ny = float(y) / H * 2.0f - 1.0f;
+    if (P.anti_aliasing) {
+        const float ox = 1.0f / W * 0.25f, oy = 1.0f / H * 0.25f;
+        const float qx[4] = {nx - ox, nx + ox, nx - ox, nx + ox};
+        const float qy[4] = {ny + oy, ny + oy, ny - oy, ny - oy};
+        V3 avg(0.0f);
+        for (int i = 0; i < 4; i++) avg += final_color(sc, P, camera_ray(cam, qx[i], qy[i]), 0, cnt);
+        avg = avg * (float)0.25;
+        return avg;
+    }
+    if (P.multiple_rays) {
+        const float ox = (1.0f / W) * (1.0f / (std::sqrt(P.sample_size) * 2));
+        const float oy = (1.0f / H) * (1.0f / (std::sqrt(P.sample_size) * 2));
+        const int moves = std::sqrt(P.sample_size) - 1;
+        const float sgn[4][2] = {{-1.0f, 1.0f}, {1.0f, 1.0f}, {-1.0f, -1.0f}, {1.0f, -1.0f}};
+        V3 avg(0.0f);
+        for (int i = 0; i < 4; i++)
+            for (int a = 1; a <= moves; a += 2)
+                for (int b = 1; b <= moves; b += 2)
+                    avg += final_color(
+                        sc, P, camera_ray(cam, nx + (ox * sgn[i][0] * a), ny + (oy * sgn[i][1] * b)), 0, cnt);
+        return avg * (float)(1.0f / P.sample_size);
+    }
+    return final_color(sc, P, camera_ray(cam, nx, ny), 0, cnt);
+}
+
+}  // namespace oracle
+
+using namespace oracle;
+
+struct oracle_scene {
+    Scene sc;
+};
+
+extern "C" {
+
+oracle_scene* oracle_create(const rt_scene_desc* d) {
+    oracle_scene* o = new oracle_scene();
+    Scene& sc = o->sc;
+    for (int m = 0; m < d->num_meshes; ++m) {
+        Mat mm;
+        mm.kd = V3::of(d->materials[m].kd);
+        mm.ks = V3::of(d->materials[m].ks);
+        mm.shininess = d->materials[m].shininess;
+        mm.transparency = d->materials[m].transparency;
+        sc.mats.push_back(mm);
+    }
+    for (int t = 0; t < d->num_triangles; ++t) {
+        std::array<Vert, 3> tri;
+        for (int c = 0; c < 3; ++c) {
+            tri[c].p = V3::of(d->positions + t * 9 + c * 3);
+            tri[c].n = V3::of(d->normals + t * 9 + c * 3);
+            if (d->texcoords) {
+                tri[c].u = d->texcoords[t * 6 + c * 2];
+                tri[c].v = d->texcoords[t * 6 + c * 2 + 1];
+            }
+        }
+        sc.tris.push_back(tri);
+        sc.tri_mesh.push_back(d->mesh_index[t]);
+    }
+    for (int s = 0; s < d->num_spheres; ++s) {
+        Sph sp;
+        sp.center = V3::of(d->spheres[s].center);
+        sp.radius = d->spheres[s].radius;
+        sp.mat.kd = V3::of(d->spheres[s].material.kd);
+        sp.mat.ks = V3::of(d->spheres[s].material.ks);
+        sp.mat.shininess = d->spheres[s].material.shininess;
+        sp.mat.transparency = d->spheres[s].material.transparency;
+        sc.spheres.push_back(sp);
+    }
+    sc.pls.assign(d->point_lights, d->point_lights + d->num_point_lights);
+    sc.sls.assign(d->spherical_lights, d->spherical_lights + d->num_spherical_lights);
+    sc.spots.assign(d->spot_lights, d->spot_lights + d->num_spot_lights);
+    sc.planes.assign(d->plane_lights, d->plane_lights + d->num_plane_lights);
+    build_bvh(sc);
+    return o;
+}
+
+void oracle_destroy(oracle_scene* o) { delete o; }
+
+int oracle_bvh_info(oracle_scene* o, int* num_nodes, int* num_leaves) {
+    *num_nodes = (int)o->sc.nodes.size();
+    int leaves = 0;
+    for (const Node& n : o->sc.nodes) leaves += n.leaf ? 1 : 0;
+    *num_leaves = leaves;
+    return 0;
+}
+
+// node boxes (lo, hi) and leaf flag, BFS creation order
+int oracle_bvh_nodes(oracle_scene* o, float* boxes, int* is_leaf, int cap) {
+    const int n = (int)o->sc.nodes.size();
+    for (int i = 0; i < n && i < cap; ++i) {
+        const Node& nd = o->sc.nodes[i];
+        const float b[6] = {nd.lo.x, nd.lo.y, nd.lo.z, nd.hi.x, nd.hi.y, nd.hi.z};
+        std::memcpy(boxes + i * 6, b, sizeof(b));
+        is_leaf[i] = nd.leaf ? 1 : 0;
+    }
+    return n;
+}
+
+int oracle_intersect(oracle_scene* o, const rt_ray* rays, int n, int use_bvh, rt_hit* out) {
+    for (int i = 0; i < n; ++i) {
+        Ray r;
+        r.origin = V3::of(rays[i].origin);
+        r.direction = V3::of(rays[i].direction);
+        r.t = rays[i].t;
+        Hit h;
+        Counter cnt;
+        const bool hit = intersect(o->sc, r, h, use_bvh != 0, cnt);
+        rt_hit& x = out[i];
+        std::memset(&x, 0, sizeof(x));
+        x.hit = hit ? 1 : 0;
+        x.t = r.t;
+        if (hit) {
+            const float nn[3] = {h.normal.x, h.normal.y, h.normal.z};
+            const float pp[3] = {h.hitPoint.x, h.hitPoint.y, h.hitPoint.z};
+            std::memcpy(x.normal, nn, 12);
+            std::memcpy(x.hit_point, pp, 12);
+            x.uv[0] = h.u;
+            x.uv[1] = h.v;
+            x.material_index = h.is_triangle ? h.material_index : -1;
+            x.prim_id = h.prim;
+            x.is_triangle = h.is_triangle ? 1 : 0;
+        } else {
+            x.material_index = -1;
+            x.prim_id = -1;
+        }
+    }
+    return 0;
+}
+
+int oracle_shade(oracle_scene* o, const rt_ray* rays, int n, const rt_params* P, float* rgb, uint64_t* counts) {
+#pragma omp parallel for schedule(dynamic, 16)
+    for (int i = 0; i < n; ++i) {
+        Ray r;
+        r.origin = V3::of(rays[i].origin);
+        r.direction = V3::of(rays[i].direction);
+        r.t = rays[i].t;
+        Counter cnt;
+        const V3 c = final_color(o->sc, *P, r, 0, cnt);
+        rgb[i * 3] = c.x;
+        rgb[i * 3 + 1] = c.y;
+        rgb[i * 3 + 2] = c.z;
+        if (counts) counts[i] = cnt.rays;
+    }
+    return 0;
+}
+
+int oracle_camera(const float look[3], const float euler[3], float dist, float fovy, float aspect, float out[9]) {
+    const Cam c = make_cam(look, euler, dist, fovy, aspect);
+    const float v[9] = {c.pos.x, c.pos.y, c.pos.z, c.qx, c.qy, c.qz, c.qw, c.hh, c.hw};
+    std::memcpy(out, v, sizeof(v));
+    return 0;
+}
+
+// Render the listed pixels (x, y pairs in renderRayTracing's y-up convention).  rgb[i] is the
+// colour setPixel(x, y, .) would store; rays[i] the intersect() calls it took.
+int oracle_render_pixels(oracle_scene* o, const float look[3], const float euler[3], float dist, float fovy,
+                         int W, int H, const rt_params* P, const int* xy, int n, float* rgb, uint64_t* rays) {
+    const Cam cam = make_cam(look, euler, dist, fovy, float(W) / float(H));
+#pragma omp parallel for schedule(dynamic, 4)
+    for (int i = 0; i < n; ++i) {
+        Counter cnt;
+        const V3 c = render_pixel(o->sc, cam, *P, W, H, xy[2 * i], xy[2 * i + 1], cnt);
+        rgb[i * 3] = c.x;
+        rgb[i * 3 + 1] = c.y;
+        rgb[i * 3 + 2] = c.z;
+        if (rays) rays[i] = cnt.rays;
+    }
+    return 0;
+}
+
+// Whole frame in Screen::m_textureData order (row (H-1-y) first), src/screen.cpp:32-38.
+int oracle_render(oracle_scene* o, const float look[3], const float euler[3], float dist, float fovy, int W, int H,
+                  const rt_params* P, float* rgb, uint64_t* total_rays) {
+    const Cam cam = make_cam(look, euler, dist, fovy, float(W) / float(H));
+    uint64_t total = 0;
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : total)
+    for (int y = 0; y < H; ++y) {
+        for (int x = 0; x < W; ++x) {
+            Counter cnt;
+            const V3 c = render_pixel(o->sc, cam, *P, W, H, x, y, cnt);
+            float* dst = rgb + ((size_t)(H - 1 - y) * W + x) * 3;
+            dst[0] = c.x;
+            dst[1] = c.y;
+            dst[2] = c.z;
+            total += cnt.rays;
+        }
+    }
+    if (total_rays) *total_rays = total;
+    return 0;
+}
+
+int oracle_set_threads(int n) {
+#ifdef _OPENMP
+    omp_set_num_threads(n);
+    return n;
+#else
+    (void)n;
+    return 1;
+#endif
+}
+}

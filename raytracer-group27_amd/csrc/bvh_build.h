@@ -1,0 +1,58 @@
+// bvh_build.h -- host-side acceleration structures.
+//
+// 1. RefBvh: the reference's own depth-capped median BVH (src/bounding_volume_hierarchy.cpp:108-366,
+//    max_level = 4 at src/bounding_volume_hierarchy.h:67).  The renderer does not traverse it for
+//    speed; it is kept because shadow rays call intersect(..., useBVH=true) (src/shadow.cpp:42) and
+//    the reference's slab test (src/ray_tracing.cpp:213-264) can reject boxes an exact test would
+//    keep.  A candidate triangle is valid for a useBVH=true query only if every box on its leaf's
+//    root path passes that slab test, and ties in t are broken by the leaf-DFS order.
+// 2. Bvh2: a binned-SAH binary BVH whose node stores both children's boxes (64 B), with leaf
+//    boxes inflated by `eps` so every point the reference's triangle test can accept lies inside.
+#pragma once
+#include <cstdint>
+#include <vector>
+
+#include "rt_math.h"
+
+namespace rt {
+
+struct RefNode {
+    v3 lower, upper;
+    bool is_leaf = false;
+    std::vector<int> children;          // node indices (inner) or object indices (leaf)
+    std::vector<uint8_t> is_triangle;   // leaf only
+};
+
+struct RefBvh {
+    std::vector<RefNode> nodes;         // BFS creation order, root = 0
+    int max_level_achieved = 0;
+    // derived
+    std::vector<int> leaf_id_of_node;   // -1 for inner nodes
+    std::vector<int> leaf_nodes;        // leaf id -> node index (leaf ids in DFS order)
+    std::vector<int> tri_key;           // triangle -> DFS visit rank (tie-break order)
+    std::vector<int> tri_leaf;          // triangle -> leaf id
+    std::vector<int> sph_key, sph_leaf;
+    std::vector<std::vector<int>> leaf_path;  // leaf id -> node indices root..leaf
+};
+
+// objects = triangles (scene order) then spheres; positions [ntri][3][3]
+RefBvh build_ref_bvh(const float* positions, int ntri, const float* sph_center_radius /*[nsph][4]*/,
+                     int nsph, int max_level = 4);
+
+struct Bvh2Node {  // 64 bytes, matches the device layout
+    float lo0[3], hi0[3], lo1[3], hi1[3];
+    int child[2];  // leaf: first triangle record; inner: node index; -1: empty
+    int count[2];  // leaf: number of records (>0); inner: 0
+};
+static_assert(sizeof(Bvh2Node) == 64, "Bvh2Node must be 64 bytes");
+
+struct Bvh2 {
+    std::vector<Bvh2Node> nodes;
+    std::vector<int> order;  // record i -> scene triangle index
+    float eps = 0.0f;
+    int max_depth = 0;
+};
+
+Bvh2 build_bvh2(const float* positions, int ntri, float eps, int max_leaf = 4);
+
+}  // namespace rt

@@ -1,0 +1,64 @@
+// host_scene.h -- host-side scene model mirroring the reference's POD types.
+//   Vertex/Material/Mesh: src/mesh.h:14-44      Scene + lights + Sphere: src/scene.h:36-94
+#pragma once
+#include <array>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "rt_math.h"
+#include "../../include/rt_amd.h"
+
+namespace rt {
+
+struct Vertex {
+    v3 p;
+    v3 n;
+    v2 uv;
+};
+
+struct Material {
+    v3 kd{0.0f, 0.0f, 0.0f};
+    v3 ks{0.0f, 0.0f, 0.0f};
+    float shininess = 1.0f;
+    float transparency = 1.0f;
+    bool has_texture = false;
+    std::string texture_path;
+};
+
+struct Mesh {
+    std::vector<Vertex> vertices;
+    std::vector<std::array<uint32_t, 3>> triangles;
+    Material material;
+};
+
+struct HostScene {
+    std::vector<Mesh> meshes;
+    std::vector<rt_sphere> spheres;
+    std::vector<rt_point_light> point_lights;
+    std::vector<rt_spherical_light> spherical_lights;
+    std::vector<rt_spot_light> spot_lights;
+    std::vector<rt_plane_light> plane_lights;
+
+    // flattened view (rebuilt by flatten())
+    std::vector<float> flat_pos, flat_nrm, flat_uv;
+    std::vector<int> flat_mesh;
+    std::vector<rt_material> flat_mat;
+    void flatten();
+    void fill_desc(rt_scene_desc* d) const;
+};
+
+// loadMesh (src/mesh.cpp:58-162) + centerAndScaleToUnitMesh (:164-188) with Assimp 5.0.1
+// OBJ/MTL importer semantics.  Throws std::runtime_error on failure.
+std::vector<Mesh> load_obj(const std::string& path, bool normalize, bool shininess_x4);
+
+// loadScene (src/scene.cpp:4-150)
+void load_preset(HostScene& scene, int preset, const std::string& data_dir, bool shininess_x4);
+
+// Deterministic torus-knot stand-in for data/dragon.obj (missing, .MISSING_LARGE_BLOBS:1)
+void write_dragon_proxy(const std::string& obj_path, int u_segments, int v_segments);
+
+// Assimp fast_atoreal_move<float> (fast_atof.h), exposed for tests.
+const char* fast_atoreal_move(const char* c, float& out, bool check_comma = true);
+
+}  // namespace rt

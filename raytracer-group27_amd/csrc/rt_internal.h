@@ -1,0 +1,12 @@
+// rt_internal.h -- shared host-side declarations between the C++ ingest code and the HIP runtime.
+#pragma once
+#include <string>
+
+namespace rt {
+void set_error(const std::string& msg);
+}
+
+#define RT_MAX_DEPTH 16        // frames of the recursion stack (reference default depth 5, configs <= 8)
+#define RT_STACK_SIZE 64       // BVH2 traversal stack entries per lane
+#define RT_MAX_REF_NODES 31    // depth-4 binary reference BVH
+#define RT_WAVE 64

@@ -1,0 +1,804 @@
+// rt_kernels.hip -- MI355X (gfx950) megakernel for the reference's per-pixel hot path.
+//
+// One lane = one pixel (one 8x8 pixel tile per 64-lane wave).  Per lane the kernel runs the
+// reference's recursion tree iteratively:
+//   renderRayTracing (src/main.cpp:340-400) -> Trackball::generateRay (framework/src/trackball.cpp:87-98)
+//   -> getFinalColor (src/main.cpp:129-301) -> BoundingVolumeHierarchy::intersect (src/bounding_volume_hierarchy.cpp:49-78)
+//   -> light gathering + cansee (src/shadow.cpp:32-321) -> calcColor (src/main.cpp:112-121)
+// Closest-hit queries walk a binned-SAH BVH2 (64-B nodes, both child boxes per node, near-first,
+// short stack in LDS) but every candidate is accepted or rejected with the reference's own
+// arithmetic (plane/edge test, src/ray_tracing.cpp:42-128; sphere quadratic in double,
+// :182-209), and ties in t go to the first object in the reference's visit order, so the hit is
+// the one the reference's brute-force loop (useBVH=false) or its depth-4 BVH walk (useBVH=true,
+// every shadow ray) returns.  useBVH=true additionally requires every box on the candidate's
+// reference leaf path to pass the reference slab test (src/ray_tracing.cpp:213-264), evaluated
+// lazily and cached per ray.
+//
+// Compiled with -ffp-contract=off (no FMA contraction), IEEE div/sqrt, f32 denormals kept.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <float.h>
+
+#include "rt_math.h"
+#include "rt_internal.h"
+
+namespace rt {
+
+struct DMat {
+    float kd[3];
+    float ks[3];
+    float shin;
+    float transp;
+};
+struct DSph {
+    float c[3];
+    float r;
+    DMat m;
+    int key_bvh;
+    int leaf;
+    int pad_[2];
+};
+struct DRefNode {
+    float lo[3];
+    float hi[3];
+};
+struct DSpot {
+    float pos[3];
+    float dir[3];
+    float cos_angle;  // std::cos(glm::radians(angle)), host constant
+    float color[3];
+};
+
+struct DevScene {
+    const float4* __restrict__ tri;      // [nrec][4] BVH2 leaf order
+    const float4* __restrict__ nodes;    // [nnodes][4]
+    const float* __restrict__ nrm;       // [ntri][9] scene order (shading normals)
+    const float* __restrict__ uv;        // [ntri][6] scene order
+    const int* __restrict__ mesh;        // [ntri] scene order
+    const DMat* __restrict__ mats;       // [nmesh]
+    const DSph* __restrict__ sph;        // [nsph]
+    const DRefNode* __restrict__ refn;   // [nref]
+    const int* __restrict__ leaf_path;   // [32][8]: count, node ids root..leaf
+    const rt_point_light* __restrict__ pl;
+    const rt_spherical_light* __restrict__ sl;
+    const DSpot* __restrict__ spot;
+    const rt_plane_light* __restrict__ plane;
+    int ntri, nsph, nref;
+    int npl, nsl, nspot, nplane;
+    int all_opaque;  // every mesh and sphere material has transparency == 1.0f
+};
+
+struct KParams {
+    DevScene S;
+    int max_level;
+    int glossy_n;
+    int plane_k;
+    int use_bvh;
+    float refr;
+    int sl_m, sl_n, sl_count;
+    float sl_sin, sl_1mcos;
+    // camera
+    float cam[3];
+    float q[4];
+    float hh, hw;
+    int W, H;
+    int aa, multi, sample_size, ms_moves;
+    float ms_offx, ms_offy;
+    float aa_offx, aa_offy;
+    // bands
+    int band_rows, band_rank, band_count, n_local_bands;
+    float* out;
+    unsigned long long* stats;  // rays, node visits, tri tests, hits
+};
+
+struct Cnt {
+    uint32_t rays, nodes, tris, hits;
+};
+
+// ------------------------------------------------------------------------------------------
+// Reference slab test (src/ray_tracing.cpp:213-264), dir = normalize(ray.direction).
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool ref_slab(const DRefNode& b, v3 o, v3 nd) {
+    if (b.lo[0] == FLT_MAX && b.lo[1] == FLT_MAX && b.lo[2] == FLT_MAX && b.hi[0] == -FLT_MAX &&
+        b.hi[1] == -FLT_MAX && b.hi[2] == -FLT_MAX)
+        return false;
+    if (o.x > b.lo[0] && o.y > b.lo[1] && o.z > b.lo[2] && o.x < b.hi[0] && o.y < b.hi[1] && o.z < b.hi[2])
+        return true;  // origin strictly inside: hit (t is restored by intersectNode)
+    const float txmin = (b.lo[0] - o.x) / nd.x;
+    const float txmax = (b.hi[0] - o.x) / nd.x;
+    const float tymin = (b.lo[1] - o.y) / nd.y;
+    const float tymax = (b.hi[1] - o.y) / nd.y;
+    const float tzmin = (b.lo[2] - o.z) / nd.z;
+    const float tzmax = (b.hi[2] - o.z) / nd.z;
+    const float tinx = (txmax < txmin) ? txmax : txmin;  // std::min
+    const float tiny = (tymax < tymin) ? tymax : tymin;
+    const float tinz = (tzmax < tzmin) ? tzmax : tzmin;
+    const float toutx = (txmin < txmax) ? txmax : txmin;  // std::max
+    const float touty = (tymin < tymax) ? tymax : tymin;
+    const float toutz = (tzmin < tzmax) ? tzmax : tzmin;
+    const float tin = gmax(gmax(tinx, tiny), tinz);
+    const float tout = gmin(gmin(toutx, touty), toutz);
+    return !(tin > tout || tout < 0.0f);
+}
+
+struct RefMask {
+    uint32_t known, pass;
+};
+
+__device__ __forceinline__ bool leaf_reachable(const DevScene& S, int leaf, v3 o, v3 nd, RefMask& m) {
+    const int* p = S.leaf_path + leaf * 8;
+    const int cnt = p[0];
+    for (int k = 1; k <= cnt; ++k) {
+        const int node = p[k];
+        const uint32_t bit = 1u << node;
+        if (!(m.known & bit)) {
+            m.known |= bit;
+            if (ref_slab(S.refn[node], o, nd)) m.pass |= bit;
+        }
+        if (!(m.pass & bit)) return false;
+    }
+    return true;
+}
+
+// ------------------------------------------------------------------------------------------
+// Closest / any hit.
+// ------------------------------------------------------------------------------------------
+struct Best {
+    float t;
+    int key;
+    int rec;  // >= 0: triangle record index; < 0: -(sphere index) - 1; INT_MIN: none
+};
+
+#define RT_NO_HIT (-0x7fffffff - 1)
+
+// Reference triangle test for one record.  Returns true and the reference t when the
+// reference would accept the triangle with ray.t = +inf (order-free part).
+__device__ __forceinline__ bool tri_test(const float4 r0, const float4 r1, const float4 r2, const float4 r3,
+                                         v3 o, v3 d, v3 nd, float& t_out) {
+    const v3 v0{r0.x, r0.y, r0.z};
+    const v3 v1{r1.x, r1.y, r1.z};
+    const v3 v2{r2.x, r2.y, r2.z};
+    const v3 n{r0.w, r1.w, r2.w};
+    const float D = r3.x;
+    // intersectRayWithPlane (src/ray_tracing.cpp:63-89)
+    const float nDotd = dot(nd, n);
+    if (nDotd == 0.0f) return false;
+    const float t = (D - dot(o, n)) / nDotd;
+    if (!(t >= 0.0f)) return false;
+    if (!(t < FLT_MAX)) return false;  // t < ray.t with the initial FLT_MAX
+    // pointInTriangle on p = o + dir * t (raw direction; src/ray_tracing.cpp:42-61,104-128)
+    const v3 p = o + d * t;
+    const bool s0 = dot(cross(p - v0, v2 - v0), n) >= 0.0f;
+    const bool s1 = dot(cross(p - v2, v1 - v2), n) >= 0.0f;
+    const bool s2 = dot(cross(p - v1, v0 - v1), n) >= 0.0f;
+    if (!((s0 && s1 && s2) || (!s0 && !s1 && !s2))) return false;
+    t_out = t;
+    return true;
+}
+
+// Sphere quadratic with the double promotions of glm::pow(float,int) (src/ray_tracing.cpp:182-209).
+__device__ __forceinline__ bool sphere_test(const DSph& s, v3 o, v3 d, float& t_out) {
+    const v3 m = o - v3{s.c[0], s.c[1], s.c[2]};
+    const float A = (float)(((double)d.x * (double)d.x + (double)d.y * (double)d.y) + (double)d.z * (double)d.z);
+    const float B = 2.0f * ((d.x * m.x + d.y * m.y) + d.z * m.z);
+    const float C = (float)((((double)m.x * (double)m.x + (double)m.y * (double)m.y) + (double)m.z * (double)m.z) -
+                            (double)s.r * (double)s.r);
+    const float disc = (float)((double)B * (double)B - (double)((4.0f * A) * C));
+    if (disc >= 0.0f) {
+        float t0 = (-B + sqrtf(disc)) / (2.0f * A);
+        float t1 = (-B - sqrtf(disc)) / (2.0f * A);
+        if (t0 < 0.0f) t0 = t1;
+        if (t1 < 0.0f) t1 = t0;
+        const float tm = gmin(t0, t1);
+        if (tm > 0.0f && tm < FLT_MAX) {
+            t_out = tm;
+            return true;
+        }
+    }
+    return false;
+}
+
+__device__ __forceinline__ v3 safe_inv(v3 d) {
+    const float e = 1e-20f;
+    const float x = fabsf(d.x) < e ? copysignf(e, d.x) : d.x;
+    const float y = fabsf(d.y) < e ? copysignf(e, d.y) : d.y;
+    const float z = fabsf(d.z) < e ? copysignf(e, d.z) : d.z;
+    return v3{1.0f / x, 1.0f / y, 1.0f / z};
+}
+
+// Conservative slab test against an inflated BVH2 child box; returns the entry distance.
+__device__ __forceinline__ bool box_hit(float lx, float ly, float lz, float hx, float hy, float hz, v3 o, v3 inv,
+                                        float tmax, float& tnear) {
+    const float ax = (lx - o.x) * inv.x, bx = (hx - o.x) * inv.x;
+    const float ay = (ly - o.y) * inv.y, by = (hy - o.y) * inv.y;
+    const float az = (lz - o.z) * inv.z, bz = (hz - o.z) * inv.z;
+    const float t0 = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+    const float t1 = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+    tnear = t0;
+    return t0 <= t1 && t1 >= 0.0f && t0 <= tmax;
+}
+
+// mode REF: useBVH=true semantics (leaf-path mask + DFS-rank tie-break)
+// ANY: any-hit with threshold `thr` (occluded iff some valid candidate has t <= thr)
+template <bool REF, bool ANY, bool COUNT>
+__device__ bool traverse(const DevScene& S, v3 o, v3 d, v3 nd, float t_init, float thr, Best& best, int* stk,
+                         Cnt& cnt) {
+    best.t = t_init;
+    best.key = -1;  // a candidate tying the caller's initial ray.t is rejected (strict t < ray.t)
+    best.rec = RT_NO_HIT;
+    RefMask mask{0u, 0u};
+    const v3 inv = safe_inv(d);
+    float tcull = ANY ? thr : t_init;
+    int sp = 0;
+    int node = 0;
+    bool found = false;
+    if (S.ntri > 0) {
+        for (;;) {
+            const float4* np = S.nodes + node * 4;
+            const float4 a = np[0];
+            const float4 b = np[1];
+            const float4 c = np[2];
+            const float4 e = np[3];
+            const int c0 = __float_as_int(e.x), c1 = __float_as_int(e.y);
+            const int n0 = __float_as_int(e.z), n1 = __float_as_int(e.w);
+            if (COUNT) cnt.nodes++;
+            float tn0 = 0.0f, tn1 = 0.0f;
+            bool h0 = (c0 >= 0) && box_hit(a.x, a.y, a.z, a.w, b.x, b.y, o, inv, tcull, tn0);
+            bool h1 = (c1 >= 0) && box_hit(b.z, b.w, c.x, c.y, c.z, c.w, o, inv, tcull, tn1);
+            // leaves are tested in place
+#pragma unroll
+            for (int side = 0; side < 2; ++side) {
+                const bool hs = side == 0 ? h0 : h1;
+                const int cnum = side == 0 ? n0 : n1;
+                const int first = side == 0 ? c0 : c1;
+                if (hs && cnum > 0) {
+                    for (int r = first; r < first + cnum; ++r) {
+                        const float4* tp = S.tri + r * 4;
+                        const float4 r0 = tp[0], r1 = tp[1], r2 = tp[2], r3 = tp[3];
+                        if (COUNT) cnt.tris++;
+                        float t;
+                        if (!tri_test(r0, r1, r2, r3, o, d, nd, t)) continue;
+                        const int key = REF ? __float_as_int(r3.z) : __float_as_int(r3.y);
+                        if (ANY) {
+                            if (!(t <= thr)) continue;
+                        } else {
+                            if (!(t < best.t || (t == best.t && key < best.key))) continue;
+                        }
+                        if (REF && !leaf_reachable(S, __float_as_int(r3.w), o, nd, mask)) continue;
+                        best.t = t;
+                        best.key = key;
+                        best.rec = r;
+                        found = true;
+                        if (ANY) return true;
+                        tcull = t;
+                    }
+                    if (side == 0) h0 = false;
+                    else h1 = false;
+                }
+            }
+            h0 = h0 && tn0 <= tcull;
+            h1 = h1 && tn1 <= tcull;
+            if (h0 && h1) {
+                const bool first0 = tn0 <= tn1;
+                stk[sp * RT_WAVE] = first0 ? c1 : c0;
+                ++sp;
+                node = first0 ? c0 : c1;
+            } else if (h0) {
+                node = c0;
+            } else if (h1) {
+                node = c1;
+            } else {
+                if (sp == 0) break;
+                --sp;
+                node = stk[sp * RT_WAVE];
+            }
+        }
+    }
+    // spheres: all tested (few); order handled by key
+    for (int s = 0; s < S.nsph; ++s) {
+        const DSph sp_ = S.sph[s];
+        float t;
+        if (!sphere_test(sp_, o, d, t)) continue;
+        const int key = REF ? sp_.key_bvh : S.ntri + s;
+        if (ANY) {
+            if (!(t <= thr)) continue;
+        } else {
+            if (!(t < best.t || (t == best.t && key < best.key))) continue;
+        }
+        if (REF && !leaf_reachable(S, sp_.leaf, o, nd, mask)) continue;
+        best.t = t;
+        best.key = key;
+        best.rec = -s - 1;
+        found = true;
+        if (ANY) return true;
+    }
+    return found;
+}
+
+// HitInfo for the winner: hitPoint, normal (interpolated + flipped), material, uv.
+struct Surf {
+    v3 p;
+    v3 n;
+    v2 uv;
+    DMat m;
+    int mesh;
+    int prim;
+    bool is_tri;
+};
+
+__device__ __forceinline__ Surf surface(const DevScene& S, v3 o, v3 d, const Best& b) {
+    Surf s;
+    if (b.rec >= 0) {
+        const float4* tp = S.tri + b.rec * 4;
+        const float4 r0 = tp[0], r1 = tp[1], r2 = tp[2], r3 = tp[3];
+        const v3 v0{r0.x, r0.y, r0.z}, v1{r1.x, r1.y, r1.z}, v2{r2.x, r2.y, r2.z};
+        const v3 fn{r0.w, r1.w, r2.w};
+        const int sidx = __float_as_int(r3.y);
+        s.p = o + d * b.t;
+        // barycentricCoordinates (src/ray_tracing.cpp:276-308), "unthresholded" semantics
+        const float A = length(cross(v1 - v0, v2 - v0));
+        v3 bc{0.0f, 0.0f, 0.0f};
+        if (A > 0.0f) {
+            bc.x = length(cross(v1 - s.p, v2 - s.p)) / A;
+            bc.y = length(cross(s.p - v0, v2 - v0)) / A;
+            bc.z = length(cross(v1 - v0, s.p - v0)) / A;
+        }
+        const float* nn = S.nrm + (size_t)sidx * 9;
+        const v3 n0{nn[0], nn[1], nn[2]}, n1{nn[3], nn[4], nn[5]}, n2{nn[6], nn[7], nn[8]};
+        v3 n = (n0 * bc.x + n1 * bc.y) + n2 * bc.z;
+        if (dot(n, fn) < 0.0f) n = -n;
+        s.n = n;
+        const float* uu = S.uv + (size_t)sidx * 6;
+        s.uv = rt::v2{(uu[0] * bc.x + uu[2] * bc.y) + uu[4] * bc.z, (uu[1] * bc.x + uu[3] * bc.y) + uu[5] * bc.z};
+        s.mesh = S.mesh[sidx];
+        s.m = S.mats[s.mesh];
+        s.prim = sidx;
+        s.is_tri = true;
+    } else {
+        const int si = -b.rec - 1;
+        const DSph sp = S.sph[si];
+        s.p = o + b.t * d;
+        s.n = normalize(s.p - v3{sp.c[0], sp.c[1], sp.c[2]});
+        s.uv = rt::v2{0.0f, 0.0f};
+        s.m = sp.m;
+        s.mesh = -1;
+        s.prim = S.ntri + si;
+        s.is_tri = false;
+    }
+    return s;
+}
+
+// ------------------------------------------------------------------------------------------
+// cansee (src/shadow.cpp:32-69): loop over transparent occluders with Fresnel attenuation.
+// ------------------------------------------------------------------------------------------
+template <bool COUNT>
+__device__ bool cansee(const DevScene& S, v3 p1, v3 p2, float& intensity, int* stk, Cnt& cnt) {
+    v3 o = p1;
+    v3 d = p2 - p1;
+    float distance = length(d);
+    d = normalize(d);
+    o = o + 0.0005f * d;
+    // d is already normalized; normalize(d) inside the triangle test is recomputed as the
+    // reference does (normalize of a unit vector is not always the identity in float).
+    const v3 nd = normalize(d);
+    while (distance > 0.0005f) {
+        cnt.rays++;
+        const float thr = distance - 2.0f * 0.0005f;
+        Best b;
+        if (S.all_opaque) {
+            // no transparent candidate can exist: occluded iff any valid candidate has t <= thr
+            return !traverse<true, true, COUNT>(S, o, d, nd, FLT_MAX, thr, b, stk, cnt);
+        }
+        const bool hit = traverse<true, false, COUNT>(S, o, d, nd, FLT_MAX, 0.0f, b, stk, cnt);
+        if (!hit || (b.t > thr)) return true;
+        const Surf s = surface(S, o, d, b);
+        if (s.m.transp != 1.0f) {
+            distance -= b.t;
+            o = s.p + 0.0005f * d;
+            const float c = fabsf(dot(d, s.n));
+            const float R0 = s.m.transp;
+            intensity = (float)((double)intensity *
+                                (1.0 - ((double)R0 + (double)(1.0f - R0) * pow((double)(1.0f - c), 5.0))));
+        } else {
+            return false;
+        }
+    }
+    return true;
+}
+
+// calcColor (src/main.cpp:112-121)
+__device__ __forceinline__ v3 calc_color(v3 lcolor, float intensity, float cosL, float cosS, const DMat& m) {
+    const v3 kd{m.kd[0], m.kd[1], m.kd[2]};
+    const v3 ks{m.ks[0], m.ks[1], m.ks[2]};
+    const v3 diffuse = ((kd * lcolor) * intensity) * cosL;
+    v3 spec{0.0f, 0.0f, 0.0f};
+    if (m.shin > 0.0f) spec = (lcolor * ks) * powf(cosS, m.shin);
+    return diffuse + spec;
+}
+
+__device__ __forceinline__ v3 ld3(const float* p) { return v3{p[0], p[1], p[2]}; }
+
+// Direct light: getPointLights, getSpherelights, getSpotLichts, getPlaneLights (src/shadow.cpp:106-321),
+// summed in that order as getFinalColor does (src/main.cpp:174-185).
+template <bool COUNT>
+__device__ v3 direct_light(const KParams& P, const Surf& s, v3 refl, int* stk, Cnt& cnt) {
+    const DevScene& S = P.S;
+    v3 color{0.0f, 0.0f, 0.0f};
+    const v3 nN = normalize(s.n);
+    const v3 nR = normalize(refl);
+    for (int i = 0; i < S.npl; ++i) {
+        const rt_point_light L = S.pl[i];
+        const v3 lp = ld3(L.position);
+        float intensity = 1.0f;
+        if (cansee<COUNT>(S, s.p, lp, intensity, stk, cnt)) {
+            const v3 ldir = normalize(lp - s.p);
+            const float cosL = fabsf(dot(nN, ldir));
+            const float dd = dot(nR, ldir);
+            const float cosS = (0.0f < dd) ? dd : 0.0f;  // std::max(0.0f, x)
+            color += calc_color(ld3(L.color), intensity, cosL, cosS, s.m);
+        }
+    }
+    for (int i = 0; i < S.nsl; ++i) {
+        const rt_spherical_light L = S.sl[i];
+        const v3 lp = ld3(L.position);
+        float intensity = 1.0f;
+        float intensitySum = 1.0f;
+        int hits = 0;
+        if (cansee<COUNT>(S, s.p, lp, intensitySum, stk, cnt)) hits++;
+        v3 dd = lp - s.p;
+        dd = normalize(dd);
+        v3 notd = dd;
+        if (dd.x != 0.0f) {
+            notd.y = -dd.x;
+            notd.x = dd.y;
+        } else {
+            notd.y = -dd.z;
+            notd.z = dd.y;
+        }
+        v3 perp = normalize(cross(dd, notd)) * L.radius;
+        const m3 rot = rodrigues(P.sl_sin, P.sl_1mcos, dd);
+        const int m = P.sl_m, n = P.sl_n;
+        for (int i2 = 0; i2 < n; ++i2) {
+            for (int j = 0; j < m; ++j) {
+                intensity = 1.0f;
+                if (cansee<COUNT>(S, s.p, lp + ((float)(m - j) / (float)m) * perp, intensity, stk, cnt)) {
+                    hits++;
+                    intensitySum += intensity;
+                }
+            }
+            perp = mul(rot, perp);
+        }
+        if (hits > 0) {
+            const float li = intensitySum / (float)P.sl_count;
+            const v3 ldir = normalize(lp - s.p);
+            const float cosL = fabsf(dot(nN, ldir));
+            const float d2 = dot(nR, ldir);
+            const float cosS = (0.0f < d2) ? d2 : 0.0f;
+            color += calc_color(ld3(L.color), li, cosL, cosS, s.m);
+        }
+    }
+    for (int i = 0; i < S.nspot; ++i) {
+        const DSpot L = S.spot[i];
+        const v3 lp = ld3(L.pos);
+        if (dot(normalize(ld3(L.dir)), normalize(s.p - lp)) > L.cos_angle) {
+            float intensity = 1.0f;
+            if (cansee<COUNT>(S, s.p, lp, intensity, stk, cnt)) {
+                const v3 ldir = normalize(lp - s.p);
+                const float cosL = fabsf(dot(nN, ldir));
+                const float d2 = dot(nR, ldir);
+                const float cosS = (0.0f < d2) ? d2 : 0.0f;
+                color += calc_color(ld3(L.color), intensity, cosL, cosS, s.m);
+            }
+        }
+    }
+    for (int i = 0; i < S.nplane; ++i) {
+        const rt_plane_light L = S.plane[i];
+        const int k = P.plane_k;
+        float hit = 0.0f;
+        int hitCount = 0;
+        float maxCos = 0.0f;
+        float intensitySum = 0.0f;
+        float intensity = 1.0f;
+        const v3 w = ld3(L.width), h = ld3(L.height), lpos = ld3(L.position);
+        const v3 dx = (1.0f / (float)(k - 1)) * w;
+        const v3 dy = (1.0f / (float)(k - 1)) * h;
+        v3 py = lpos;
+        const v3 normal = normalize(cross(w, h));
+        if (dot(normalize(s.p - (lpos + 0.5f * (w + h))), normal) > 0.0f) {
+            for (int i2 = 0; i2 < k; ++i2) {
+                v3 px = py;
+                for (int j = 0; j < k; ++j) {
+                    intensity = 1.0f;
+                    if (cansee<COUNT>(S, s.p, px, intensity, stk, cnt)) {
+                        intensitySum += intensity;
+                        const float dn = dot(normalize(s.p - px), normal);
+                        hit += ((dn < 0.0f) ? 0.0f : dn) / length(s.p - px);
+                        hitCount++;
+                        const float c2 = dot(nR, normalize(px - s.p));
+                        maxCos = (maxCos < c2) ? c2 : maxCos;
+                    }
+                    px = px + dx;
+                }
+                py = py + dy;
+            }
+        }
+        if (hit > 0.0f) {
+            const float li = (intensitySum / (float)hitCount) * hit / (float)(k * k);
+            color += calc_color(ld3(L.color), li, 1.0f, maxCos, s.m);
+        }
+    }
+    return color;
+}
+
+// ------------------------------------------------------------------------------------------
+// getFinalColor as an iterative depth-first walk of its recursion tree.  Each frame keeps the
+// parent's partial colour so children are folded in with the reference's exact nesting:
+//   mirror:      color += (ks * (0 + ks * child)) / glossy_ray_count   (or ks * (...) if shininess == 0)
+//   transparent: color += R * reflectChild;  color += (1-R) * refractChild   (src/main.cpp:191-290)
+// ------------------------------------------------------------------------------------------
+enum { FR_MIRROR = 0, FR_TRANS_A = 1, FR_TRANS_B = 2 };
+struct Frame {
+    v3 color;
+    v3 w;      // ks (mirror) | (reflectionChance, refractionChance, -) (transparent)
+    v3 o2, d2; // pending refracted ray
+    int mode;
+    int flag;  // mirror: shininess != 0 ; transparent: refracted ray traced
+};
+
+template <bool COUNT>
+__device__ v3 get_final_color(const KParams& P, v3 o, v3 d, float t_init, int* stk, Cnt& cnt) {
+    const DevScene& S = P.S;
+    Frame fr[RT_MAX_DEPTH];
+    int level = 0;
+    for (;;) {
+        v3 col{0.0f, 0.0f, 0.0f};
+        bool descend = false;
+        cnt.rays++;
+        Best b;
+        const v3 nd = normalize(d);
+        bool hit = P.use_bvh ? traverse<true, false, COUNT>(S, o, d, nd, t_init, 0.0f, b, stk, cnt)
+                             : traverse<false, false, COUNT>(S, o, d, nd, t_init, 0.0f, b, stk, cnt);
+        t_init = FLT_MAX;
+        if (hit) {
+            if (COUNT) cnt.hits++;
+            const Surf s = surface(S, o, d, b);
+            const v3 refl = reflect(normalize(d), normalize(s.n));
+            col = direct_light<COUNT>(P, s, refl, stk, cnt);
+            if (level < P.max_level) {
+                if (s.m.transp == 1.0f) {
+                    if (s.m.ks[0] > 0.0f || s.m.ks[1] > 0.0f || s.m.ks[2] > 0.0f) {
+                        Frame& f = fr[level];
+                        f.color = col;
+                        f.w = v3{s.m.ks[0], s.m.ks[1], s.m.ks[2]};
+                        f.mode = FR_MIRROR;
+                        f.flag = (s.m.shin != 0.0f);
+                        o = s.p + 0.01f * refl;
+                        d = refl;
+                        descend = true;
+                    }
+                } else {
+                    const v3 l = normalize(d);
+                    const v3 n = normalize(s.n);
+                    const float r = P.refr;
+                    const float c = fabsf(dot(l, n));
+                    v3 refr = r * l + (r * c - sqrtf(1.0f - r * r * (1.0f - c * c))) * n;
+                    refr = normalize(refr);
+                    const float R0 = s.m.transp;
+                    const float reflC = (float)((double)R0 + (double)(1.0f - R0) * pow((double)(1.0f - c), 5.0));
+                    const float refrC = 1.0f - reflC;
+                    Frame& f = fr[level];
+                    f.color = col;
+                    f.w = v3{reflC, refrC, 0.0f};
+                    f.o2 = s.p + 0.01f * refr;
+                    f.d2 = refr;
+                    f.mode = FR_TRANS_A;
+                    f.flag = (r * r * (1.0f - c * c) <= 1.0f);
+                    o = s.p + 0.01f * refl;
+                    d = refl;
+                    descend = true;
+                }
+            }
+        }
+        if (descend) {
+            ++level;
+            continue;
+        }
+        v3 child = col;
+        bool resumed = false;
+        while (level > 0) {
+            --level;
+            Frame& f = fr[level];
+            if (f.mode == FR_MIRROR) {
+                const v3 rc = v3{0.0f, 0.0f, 0.0f} + f.w * child;
+                const v3 add = f.flag ? (f.w * rc) / (float)P.glossy_n : f.w * rc;
+                child = f.color + add;
+            } else if (f.mode == FR_TRANS_A) {
+                f.color = f.color + f.w.x * child;
+                if (f.flag) {
+                    f.mode = FR_TRANS_B;
+                    o = f.o2;
+                    d = f.d2;
+                    ++level;
+                    resumed = true;
+                    break;
+                }
+                child = f.color;
+            } else {
+                child = f.color + f.w.y * child;
+            }
+        }
+        if (!resumed) return child;
+    }
+}
+
+__device__ __forceinline__ void gen_ray(const KParams& P, float px, float py, v3& o, v3& d) {
+    const v3 csd = normalize(v3{-px * P.hw, py * P.hh, 1.0f});
+    o = v3{P.cam[0], P.cam[1], P.cam[2]};
+    d = quat_rotate(P.q[0], P.q[1], P.q[2], P.q[3], csd);
+}
+
+template <bool COUNT>
+__device__ void flush_counters(const KParams& P, const Cnt& c) {
+    // wave-level reduction, one atomic per wave and counter
+    unsigned long long r = c.rays, nv = c.nodes, tt = c.tris, h = c.hits;
+    for (int off = 32; off > 0; off >>= 1) {
+        r += __shfl_xor(r, off);
+        if (COUNT) {
+            nv += __shfl_xor(nv, off);
+            tt += __shfl_xor(tt, off);
+            h += __shfl_xor(h, off);
+        }
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(P.stats + 0, r);
+        if (COUNT) {
+            atomicAdd(P.stats + 1, nv);
+            atomicAdd(P.stats + 2, tt);
+            atomicAdd(P.stats + 3, h);
+        }
+    }
+}
+
+// One 64-lane block renders one 8x8 pixel tile of one band.
+template <bool COUNT>
+__global__ __launch_bounds__(64) void render_kernel(KParams P) {
+    __shared__ int stack_lds[RT_STACK_SIZE * RT_WAVE];
+    const int lane = threadIdx.x;
+    int* stk = stack_lds + lane;
+    const int tiles_x = (P.W + 7) / 8;
+    const int tiles_y_band = (P.band_rows + 7) / 8;
+    const int tile = blockIdx.x;
+    const int tx = tile % tiles_x;
+    const int rest = tile / tiles_x;
+    const int ty = rest % tiles_y_band;
+    const int lb = rest / tiles_y_band;  // local band
+    const int gb = lb * P.band_count + P.band_rank;
+    const int row_in_band = ty * 8 + (lane >> 3);
+    const int x = tx * 8 + (lane & 7);
+    const int y = gb * P.band_rows + row_in_band;
+    Cnt cnt{0u, 0u, 0u, 0u};
+    const bool active = (x < P.W) && (row_in_band < P.band_rows) && (y < P.H) && (lb < P.n_local_bands);
+    if (active) {
+        const float ndx = (float)x / (float)P.W * 2.0f - 1.0f;
+        const float ndy = (float)y / (float)P.H * 2.0f - 1.0f;
+        v3 col;
+        v3 o, d;
+        if (P.aa) {
+            const float sx[4] = {ndx - P.aa_offx, ndx + P.aa_offx, ndx - P.aa_offx, ndx + P.aa_offx};
+            const float sy[4] = {ndy + P.aa_offy, ndy + P.aa_offy, ndy - P.aa_offy, ndy - P.aa_offy};
+            v3 acc{0.0f, 0.0f, 0.0f};
+            for (int i = 0; i < 4; ++i) {
+                gen_ray(P, sx[i], sy[i], o, d);
+                acc += get_final_color<COUNT>(P, o, d, FLT_MAX, stk, cnt);
+            }
+            col = acc * 0.25f;
+        } else if (P.multi) {
+            const float qs[4][2] = {{-1.0f, 1.0f}, {1.0f, 1.0f}, {-1.0f, -1.0f}, {1.0f, -1.0f}};
+            v3 acc{0.0f, 0.0f, 0.0f};
+            for (int i = 0; i < 4; ++i)
+                for (int xx = 1; xx <= P.ms_moves; xx += 2)
+                    for (int yy = 1; yy <= P.ms_moves; yy += 2) {
+                        const float rx = ndx + (P.ms_offx * qs[i][0] * (float)xx);
+                        const float ry = ndy + (P.ms_offy * qs[i][1] * (float)yy);
+                        gen_ray(P, rx, ry, o, d);
+                        acc += get_final_color<COUNT>(P, o, d, FLT_MAX, stk, cnt);
+                    }
+            col = acc * (float)(1.0f / (float)P.sample_size);
+        } else {
+            gen_ray(P, ndx, ndy, o, d);
+            col = get_final_color<COUNT>(P, o, d, FLT_MAX, stk, cnt);
+        }
+        float* dst = P.out + (((size_t)lb * P.band_rows + row_in_band) * P.W + x) * 3;
+        dst[0] = col.x;
+        dst[1] = col.y;
+        dst[2] = col.z;
+    }
+    flush_counters<COUNT>(P, cnt);
+}
+
+// Per-ray kernels for rt_intersect / rt_shade.
+__global__ __launch_bounds__(64) void intersect_kernel(KParams P, const rt_ray* rays, int n, int use_bvh, rt_hit* hits) {
+    __shared__ int stack_lds[RT_STACK_SIZE * RT_WAVE];
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    int* stk = stack_lds + threadIdx.x;
+    if (i >= n) return;
+    const rt_ray r = rays[i];
+    const v3 o{r.origin[0], r.origin[1], r.origin[2]};
+    const v3 d{r.direction[0], r.direction[1], r.direction[2]};
+    const v3 nd = normalize(d);
+    Best b;
+    Cnt cnt{0u, 0u, 0u, 0u};
+    const bool hit = use_bvh ? traverse<true, false, false>(P.S, o, d, nd, r.t, 0.0f, b, stk, cnt)
+                             : traverse<false, false, false>(P.S, o, d, nd, r.t, 0.0f, b, stk, cnt);
+    rt_hit h;
+    h.hit = hit ? 1 : 0;
+    h.t = hit ? b.t : r.t;
+    if (hit) {
+        const Surf s = surface(P.S, o, d, b);
+        h.normal[0] = s.n.x;
+        h.normal[1] = s.n.y;
+        h.normal[2] = s.n.z;
+        h.hit_point[0] = s.p.x;
+        h.hit_point[1] = s.p.y;
+        h.hit_point[2] = s.p.z;
+        h.uv[0] = s.uv.x;
+        h.uv[1] = s.uv.y;
+        h.material_index = s.mesh;
+        h.prim_id = s.prim;
+        h.is_triangle = s.is_tri ? 1 : 0;
+    } else {
+        for (int k = 0; k < 3; ++k) h.normal[k] = h.hit_point[k] = 0.0f;
+        h.uv[0] = h.uv[1] = 0.0f;
+        h.material_index = -1;
+        h.prim_id = -1;
+        h.is_triangle = 0;
+    }
+    hits[i] = h;
+}
+
+__global__ __launch_bounds__(64) void shade_kernel(KParams P, const rt_ray* rays, int n, float* rgb,
+                                                   unsigned long long* ray_counts) {
+    __shared__ int stack_lds[RT_STACK_SIZE * RT_WAVE];
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    int* stk = stack_lds + threadIdx.x;
+    if (i >= n) return;
+    const rt_ray r = rays[i];
+    Cnt cnt{0u, 0u, 0u, 0u};
+    const v3 c = get_final_color<false>(P, v3{r.origin[0], r.origin[1], r.origin[2]},
+                                        v3{r.direction[0], r.direction[1], r.direction[2]}, r.t, stk, cnt);
+    rgb[i * 3 + 0] = c.x;
+    rgb[i * 3 + 1] = c.y;
+    rgb[i * 3 + 2] = c.z;
+    ray_counts[i] = cnt.rays;
+}
+
+// Gathered band buffers [band_count][max_local][band_rows][W][3] -> setPixel layout
+// (src/screen.cpp:32-38: index (H-1-y)*W + x).
+__global__ void unpermute_kernel(int W, int H, int band_rows, int band_count, int max_local, const float* src,
+                                 float* dst) {
+    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t total = (size_t)W * H;
+    if (idx >= total) return;
+    const int x = (int)(idx % W);
+    const int y = (int)(idx / W);
+    const int gb = y / band_rows;
+    const int r = y % band_rows;
+    const int rank = gb % band_count;
+    const int lb = gb / band_count;
+    const float* s = src + ((((size_t)rank * max_local + lb) * band_rows + r) * W + x) * 3;
+    float* d = dst + ((size_t)(H - 1 - y) * W + x) * 3;
+    d[0] = s[0];
+    d[1] = s[1];
+    d[2] = s[2];
+}
+
+__global__ void selftest_kernel(const float* x, const float* y, int n, float* out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out[i * 4 + 0] = sqrtf(x[i]);
+    out[i * 4 + 1] = 1.0f / x[i];
+    out[i * 4 + 2] = x[i] / y[i];
+    out[i * 4 + 3] = powf(x[i], y[i]);
+}
+
+}  // namespace rt

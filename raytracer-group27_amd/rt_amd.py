@@ -1,0 +1,427 @@
+"""ctypes binding of librt_amd.so (include/rt_amd.h) + the C1..C5 config manifest.
+
+Host-side mirror of the reference interface for the hot path: Scene / loadScene / loadMesh,
+BoundingVolumeHierarchy(Scene*) + intersect(), getFinalColor(), renderRayTracing().  The
+product path is the HIP library; if it cannot be loaded this module raises -- there is no CPU
+fallback.
+"""
+import ctypes as C
+import gzip
+import os
+import shutil
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+LIB_PATH = os.path.join(HERE, "librt_amd.so")
+SCENE_DIR = os.path.join(REPO, "tests", "golden", "scenes")
+
+FLT_MAX = float(np.finfo(np.float32).max)
+
+
+class rt_material(C.Structure):
+    _fields_ = [("kd", C.c_float * 3), ("ks", C.c_float * 3), ("shininess", C.c_float),
+                ("transparency", C.c_float), ("has_texture", C.c_int), ("pad_", C.c_int)]
+
+
+class rt_sphere(C.Structure):
+    _fields_ = [("center", C.c_float * 3), ("radius", C.c_float), ("material", rt_material)]
+
+
+class rt_point_light(C.Structure):
+    _fields_ = [("position", C.c_float * 3), ("color", C.c_float * 3)]
+
+
+class rt_spherical_light(C.Structure):
+    _fields_ = [("position", C.c_float * 3), ("radius", C.c_float), ("color", C.c_float * 3)]
+
+
+class rt_spot_light(C.Structure):
+    _fields_ = [("position", C.c_float * 3), ("direction", C.c_float * 3), ("angle", C.c_float),
+                ("color", C.c_float * 3)]
+
+
+class rt_plane_light(C.Structure):
+    _fields_ = [("position", C.c_float * 3), ("width", C.c_float * 3), ("height", C.c_float * 3),
+                ("color", C.c_float * 3)]
+
+
+class rt_scene_desc(C.Structure):
+    _fields_ = [("num_triangles", C.c_int), ("positions", C.POINTER(C.c_float)),
+                ("normals", C.POINTER(C.c_float)), ("texcoords", C.POINTER(C.c_float)),
+                ("mesh_index", C.POINTER(C.c_int)), ("num_meshes", C.c_int),
+                ("materials", C.POINTER(rt_material)), ("num_spheres", C.c_int),
+                ("spheres", C.POINTER(rt_sphere)), ("num_point_lights", C.c_int),
+                ("point_lights", C.POINTER(rt_point_light)), ("num_spherical_lights", C.c_int),
+                ("spherical_lights", C.POINTER(rt_spherical_light)), ("num_spot_lights", C.c_int),
+                ("spot_lights", C.POINTER(rt_spot_light)), ("num_plane_lights", C.c_int),
+                ("plane_lights", C.POINTER(rt_plane_light))]
+
+
+class rt_camera(C.Structure):
+    _fields_ = [("position", C.c_float * 3), ("quat", C.c_float * 4), ("half_height", C.c_float),
+                ("half_width", C.c_float)]
+
+
+class rt_params(C.Structure):
+    _fields_ = [("max_reflection_level", C.c_int), ("sphere_light_ray_count", C.c_int),
+                ("plane_light_1D_ray_count", C.c_int), ("glossy_ray_count", C.c_int),
+                ("refraction_factor", C.c_float), ("use_bvh", C.c_int), ("anti_aliasing", C.c_int),
+                ("multiple_rays", C.c_int), ("sample_size", C.c_int), ("barycentric_mode", C.c_int),
+                ("rng_seed", C.c_uint64)]
+
+
+class rt_ray(C.Structure):
+    _fields_ = [("origin", C.c_float * 3), ("direction", C.c_float * 3), ("t", C.c_float)]
+
+
+class rt_hit(C.Structure):
+    _fields_ = [("hit", C.c_int), ("t", C.c_float), ("normal", C.c_float * 3), ("hit_point", C.c_float * 3),
+                ("uv", C.c_float * 2), ("material_index", C.c_int), ("prim_id", C.c_int),
+                ("is_triangle", C.c_int)]
+
+
+class rt_stats(C.Structure):
+    _fields_ = [("rays", C.c_uint64), ("node_visits", C.c_uint64), ("tri_tests", C.c_uint64),
+                ("hits", C.c_uint64), ("kernel_ms", C.c_float), ("pad_", C.c_float)]
+
+
+RAY_DTYPE = np.dtype([("origin", "<f4", 3), ("direction", "<f4", 3), ("t", "<f4")])
+HIT_DTYPE = np.dtype([("hit", "<i4"), ("t", "<f4"), ("normal", "<f4", 3), ("hit_point", "<f4", 3),
+                      ("uv", "<f4", 2), ("material_index", "<i4"), ("prim_id", "<i4"), ("is_triangle", "<i4")])
+assert RAY_DTYPE.itemsize == C.sizeof(rt_ray) and HIT_DTYPE.itemsize == C.sizeof(rt_hit)
+
+# Every symbol include/rt_amd.h declares (checked by tests/test_abi.py).
+EXPORTS = [
+    "rt_abi_version", "rt_last_error", "rt_scene_new", "rt_scene_load_obj", "rt_scene_preset",
+    "rt_scene_add_sphere", "rt_scene_add_point_light", "rt_scene_add_spherical_light",
+    "rt_scene_add_spot_light", "rt_scene_add_plane_light", "rt_scene_clear_lights", "rt_scene_set_material",
+    "rt_scene_desc_get", "rt_scene_free", "rt_write_dragon_proxy", "rt_camera_from_trackball", "rt_create",
+    "rt_destroy", "rt_render", "rt_render_device", "rt_unpermute_bands_device", "rt_intersect", "rt_shade",
+    "rt_set_counting", "rt_ctx_info", "rt_selftest_math",
+]
+
+_lib = None
+
+
+def lib():
+    """Load librt_amd.so (raises if it is missing: the product has no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: run __graft_entry__.build() (HIP path has no fallback)")
+        L = C.CDLL(LIB_PATH)
+        P = C.POINTER
+        vp = C.c_void_p
+        sigs = {
+            "rt_abi_version": ([], C.c_int),
+            "rt_last_error": ([C.c_char_p, C.c_size_t], C.c_int),
+            "rt_scene_new": ([P(vp)], C.c_int),
+            "rt_scene_load_obj": ([vp, C.c_char_p, C.c_int, C.c_int], C.c_int),
+            "rt_scene_preset": ([vp, C.c_int, C.c_char_p, C.c_int], C.c_int),
+            "rt_scene_add_sphere": ([vp, P(rt_sphere)], C.c_int),
+            "rt_scene_add_point_light": ([vp, P(rt_point_light)], C.c_int),
+            "rt_scene_add_spherical_light": ([vp, P(rt_spherical_light)], C.c_int),
+            "rt_scene_add_spot_light": ([vp, P(rt_spot_light)], C.c_int),
+            "rt_scene_add_plane_light": ([vp, P(rt_plane_light)], C.c_int),
+            "rt_scene_clear_lights": ([vp], C.c_int),
+            "rt_scene_set_material": ([vp, C.c_int, P(rt_material)], C.c_int),
+            "rt_scene_desc_get": ([vp, P(rt_scene_desc)], C.c_int),
+            "rt_scene_free": ([vp], C.c_int),
+            "rt_write_dragon_proxy": ([C.c_char_p, C.c_int, C.c_int], C.c_int),
+            "rt_camera_from_trackball": ([P(C.c_float), P(C.c_float), C.c_float, C.c_float, C.c_float,
+                                         P(rt_camera)], C.c_int),
+            "rt_create": ([P(rt_scene_desc), C.c_int, P(vp)], C.c_int),
+            "rt_destroy": ([vp], C.c_int),
+            "rt_render": ([vp, P(rt_camera), P(rt_params), C.c_int, C.c_int, P(C.c_float), P(rt_stats)], C.c_int),
+            "rt_render_device": ([vp, P(rt_camera), P(rt_params), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                  vp, vp, P(rt_stats)], C.c_int),
+            "rt_unpermute_bands_device": ([C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp], C.c_int),
+            "rt_intersect": ([vp, vp, C.c_int, C.c_int, vp], C.c_int),
+            "rt_shade": ([vp, vp, C.c_int, P(rt_params), P(C.c_float), P(C.c_uint64)], C.c_int),
+            "rt_set_counting": ([C.c_int], C.c_int),
+            "rt_ctx_info": ([vp, P(C.c_int), P(C.c_int), P(C.c_int), P(C.c_int)], C.c_int),
+            "rt_selftest_math": ([vp, P(C.c_float), P(C.c_float), C.c_int, P(C.c_float)], C.c_int),
+        }
+        for name, (args, res) in sigs.items():
+            f = getattr(L, name)
+            f.argtypes = args
+            f.restype = res
+        _lib = L
+    return _lib
+
+
+class RtError(RuntimeError):
+    pass
+
+
+def check(rc, what=""):
+    if rc != 0:
+        buf = C.create_string_buffer(1024)
+        lib().rt_last_error(buf, 1024)
+        raise RtError(f"{what} failed ({rc}): {buf.value.decode(errors='replace')}")
+
+
+def _f3(v):
+    return (C.c_float * 3)(*[float(np.float32(x)) for x in v])
+
+
+def material(kd, ks=(0, 0, 0), shininess=1.0, transparency=1.0):
+    """Material{kd, ks{0}, shininess{1}, transparency{1}} (src/mesh.h:23-33)."""
+    return rt_material(_f3(kd), _f3(ks), float(np.float32(shininess)), float(np.float32(transparency)), 0, 0)
+
+
+class Scene:
+    """Scene + loadScene/loadMesh (src/scene.cpp:4-150, src/mesh.cpp:58-188)."""
+
+    def __init__(self):
+        self.h = C.c_void_p()
+        check(lib().rt_scene_new(C.byref(self.h)), "rt_scene_new")
+
+    def __del__(self):
+        if getattr(self, "h", None) and self.h.value:
+            lib().rt_scene_free(self.h)
+            self.h = C.c_void_p()
+
+    def load_obj(self, path, normalize=False, shininess_x4=False):
+        check(lib().rt_scene_load_obj(self.h, str(path).encode(), int(normalize), int(shininess_x4)),
+              f"loadMesh({path})")
+        return self
+
+    def preset(self, preset, data_dir, shininess_x4=False):
+        check(lib().rt_scene_preset(self.h, int(preset), str(data_dir).encode(), int(shininess_x4)),
+              f"loadScene({preset})")
+        return self
+
+    def add_sphere(self, center, radius, mat):
+        s = rt_sphere(_f3(center), float(np.float32(radius)), mat)
+        check(lib().rt_scene_add_sphere(self.h, C.byref(s)))
+
+    def add_point_light(self, pos, color):
+        check(lib().rt_scene_add_point_light(self.h, C.byref(rt_point_light(_f3(pos), _f3(color)))))
+
+    def add_spherical_light(self, pos, radius, color):
+        l = rt_spherical_light(_f3(pos), float(np.float32(radius)), _f3(color))
+        check(lib().rt_scene_add_spherical_light(self.h, C.byref(l)))
+
+    def add_spot_light(self, pos, direction, angle, color):
+        l = rt_spot_light(_f3(pos), _f3(direction), float(np.float32(angle)), _f3(color))
+        check(lib().rt_scene_add_spot_light(self.h, C.byref(l)))
+
+    def add_plane_light(self, pos, width, height, color):
+        l = rt_plane_light(_f3(pos), _f3(width), _f3(height), _f3(color))
+        check(lib().rt_scene_add_plane_light(self.h, C.byref(l)))
+
+    def clear_lights(self):
+        check(lib().rt_scene_clear_lights(self.h))
+
+    def set_material(self, mesh, mat):
+        check(lib().rt_scene_set_material(self.h, int(mesh), C.byref(mat)), "set_material")
+
+    def desc(self):
+        d = rt_scene_desc()
+        check(lib().rt_scene_desc_get(self.h, C.byref(d)), "rt_scene_desc_get")
+        return d
+
+    def arrays(self):
+        """numpy copies of the flat scene (positions [T,3,3], normals [T,3,3], mesh [T], materials)."""
+        d = self.desc()
+        T = d.num_triangles
+        pos = np.ctypeslib.as_array(d.positions, shape=(T * 9,)).reshape(T, 3, 3).copy() if T else np.zeros((0, 3, 3), np.float32)
+        nrm = np.ctypeslib.as_array(d.normals, shape=(T * 9,)).reshape(T, 3, 3).copy() if T else np.zeros((0, 3, 3), np.float32)
+        mesh = np.ctypeslib.as_array(d.mesh_index, shape=(T,)).copy() if T else np.zeros((0,), np.int32)
+        mats = [d.materials[i] for i in range(d.num_meshes)]
+        return pos, nrm, mesh, mats
+
+
+def camera_from_trackball(look_at=(0.0, 0.0, 0.0), euler=None, distance=3.0, fovy=None, aspect=1.0):
+    """Trackball::position/generateRay constants (framework/src/trackball.cpp:65-98)."""
+    if euler is None:
+        euler = default_euler()
+    if fovy is None:
+        fovy = default_fovy()
+    cam = rt_camera()
+    la = (C.c_float * 3)(*look_at)
+    eu = (C.c_float * 3)(*euler)
+    check(lib().rt_camera_from_trackball(la, eu, float(np.float32(distance)), float(np.float32(fovy)),
+                                         float(np.float32(aspect)), C.byref(cam)), "camera")
+    return cam
+
+
+RADIANS = np.float32(0.01745329251994329576923690768489)
+
+
+def default_euler():
+    """glm::radians(glm::vec3(20.0f, 20.0f, 0.0f)) (src/main.cpp:414), float32 multiply."""
+    return [float(np.float32(20.0) * RADIANS), float(np.float32(20.0) * RADIANS), float(np.float32(0.0) * RADIANS)]
+
+
+def default_fovy():
+    """glm::radians(50.0f) (src/main.cpp:413)."""
+    return float(np.float32(50.0) * RADIANS)
+
+
+def aspect_of(W, H):
+    """Window::aspectRatio() = float(w)/float(h) (framework/src/window.cpp:334-337)."""
+    return float(np.float32(W) / np.float32(H))
+
+
+def params(max_reflection_level=5, sphere_light_ray_count=10, plane_light_1D_ray_count=3, glossy_ray_count=10,
+           refraction_factor=0.8, use_bvh=False, anti_aliasing=False, multiple_rays=False, sample_size=4, seed=0x5EED):
+    """Render knobs with the reference defaults (src/main.cpp:54-64,123-127)."""
+    return rt_params(max_reflection_level, sphere_light_ray_count, plane_light_1D_ray_count, glossy_ray_count,
+                     float(np.float32(refraction_factor)), int(use_bvh), int(anti_aliasing), int(multiple_rays),
+                     sample_size, 0, seed)
+
+
+class Context:
+    """Device context = BoundingVolumeHierarchy(Scene*) + uploaded scene (one GPU)."""
+
+    def __init__(self, scene, device=0):
+        self.scene = scene  # keep the host scene alive (desc points into it)
+        self.h = C.c_void_p()
+        d = scene.desc()
+        check(lib().rt_create(C.byref(d), int(device), C.byref(self.h)), "rt_create")
+
+    def close(self):
+        if getattr(self, "h", None) and self.h.value:
+            lib().rt_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        self.close()
+
+    def info(self):
+        a, b, c, d = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+        check(lib().rt_ctx_info(self.h, C.byref(a), C.byref(b), C.byref(c), C.byref(d)))
+        return {"bvh_nodes": a.value, "tri_records": b.value, "ref_bvh_nodes": c.value, "ref_bvh_levels": d.value}
+
+    def render(self, cam, prm, W, H):
+        """renderRayTracing: returns (float32 [H*W*3] in Screen::m_textureData order, rt_stats)."""
+        out = np.empty(W * H * 3, np.float32)
+        st = rt_stats()
+        check(lib().rt_render(self.h, C.byref(cam), C.byref(prm), W, H,
+                              out.ctypes.data_as(C.POINTER(C.c_float)), C.byref(st)), "rt_render")
+        return out, st
+
+    def render_device(self, cam, prm, W, H, band_rows, band_rank, band_count, d_out_ptr, stream_ptr=None):
+        st = rt_stats()
+        check(lib().rt_render_device(self.h, C.byref(cam), C.byref(prm), W, H, band_rows, band_rank, band_count,
+                                     C.c_void_p(d_out_ptr), C.c_void_p(stream_ptr or 0), C.byref(st)),
+              "rt_render_device")
+        return st
+
+    def intersect(self, rays, use_bvh):
+        rays = np.ascontiguousarray(rays, dtype=RAY_DTYPE)
+        hits = np.zeros(len(rays), HIT_DTYPE)
+        check(lib().rt_intersect(self.h, rays.ctypes.data, len(rays), int(use_bvh), hits.ctypes.data), "rt_intersect")
+        return hits
+
+    def shade(self, rays, prm):
+        rays = np.ascontiguousarray(rays, dtype=RAY_DTYPE)
+        rgb = np.zeros(len(rays) * 3, np.float32)
+        cnt = np.zeros(len(rays), np.uint64)
+        check(lib().rt_shade(self.h, rays.ctypes.data, len(rays), C.byref(prm),
+                             rgb.ctypes.data_as(C.POINTER(C.c_float)),
+                             cnt.ctypes.data_as(C.POINTER(C.c_uint64))), "rt_shade")
+        return rgb.reshape(-1, 3), cnt
+
+    def selftest_math(self, x, y):
+        x = np.ascontiguousarray(x, np.float32)
+        y = np.ascontiguousarray(y, np.float32)
+        out = np.zeros(len(x) * 4, np.float32)
+        check(lib().rt_selftest_math(self.h, x.ctypes.data_as(C.POINTER(C.c_float)),
+                                     y.ctypes.data_as(C.POINTER(C.c_float)), len(x),
+                                     out.ctypes.data_as(C.POINTER(C.c_float))))
+        return out.reshape(-1, 4)
+
+
+def set_counting(on):
+    check(lib().rt_set_counting(int(on)))
+
+
+# --------------------------------------------------------------------------------------------
+# Scene data: the reference's data/*.obj/.mtl inputs ship gzip-compressed under
+# tests/golden/scenes/ and are expanded into a cache dir (the GPU box has no /root/reference).
+# --------------------------------------------------------------------------------------------
+def cache_dir():
+    d = os.environ.get("RT_SCENE_CACHE") or os.path.join(tempfile.gettempdir(), f"rt_amd_scenes_{os.getuid()}")
+    os.makedirs(d, exist_ok=True)
+    return d
+
+
+def data_dir():
+    """Directory holding the expanded reference scene files (tr_def, cube, monkey, Cornell)."""
+    out = cache_dir()
+    for f in sorted(os.listdir(SCENE_DIR)):
+        if not f.endswith(".gz"):
+            continue
+        dst = os.path.join(out, f[:-3])
+        src = os.path.join(SCENE_DIR, f)
+        if not os.path.exists(dst) or os.path.getmtime(dst) < os.path.getmtime(src):
+            with gzip.open(src, "rb") as fi, open(dst + ".tmp", "wb") as fo:
+                shutil.copyfileobj(fi, fo)
+            os.replace(dst + ".tmp", dst)
+    return out
+
+
+DRAGON_U, DRAGON_V = 1000, 400  # 800 000 triangles
+
+
+def dragon_proxy_path(u=DRAGON_U, v=DRAGON_V):
+    path = os.path.join(cache_dir(), f"dragon_proxy_{u}x{v}.obj")
+    if not os.path.exists(path):
+        tmp = path + f".{os.getpid()}.obj"
+        check(lib().rt_write_dragon_proxy(tmp.encode(), u, v), "rt_write_dragon_proxy")
+        mtl_tmp = tmp[:-4] + ".mtl"
+        # the .obj names its .mtl by basename: rewrite both to the final names
+        with open(tmp) as f:
+            text = f.read().replace(os.path.basename(mtl_tmp), os.path.basename(path)[:-4] + ".mtl", 1)
+        with open(tmp, "w") as f:
+            f.write(text)
+        os.replace(mtl_tmp, path[:-4] + ".mtl")
+        os.replace(tmp, path)
+    return path
+
+
+# SceneType (src/scene.h:14-34)
+PRESETS = {"SingleTriangle": 0, "Bookeshelf": 1, "Cube": 2, "CornellBox": 3, "CornellBoxSphericalLight": 4,
+           "CornellBoxPlaneLight": 5, "Monkey": 6, "Teapot": 7, "Dragon": 8, "Spheres": 9, "ChessBoard": 10,
+           "Custom": 11, "AndreasScene": 12, "CatalinScene": 13, "MikeScene": 14, "MikeScene2": 15}
+
+
+def build_config(name, dragon_uv=None):
+    """BASELINE.json configs as fixed by SURVEY.md §8d.  Returns (scene, params, W, H, description)."""
+    dd = data_dir()
+    s = Scene()
+    if name == "C1":
+        s.load_obj(os.path.join(dd, "cube.obj"), normalize=False)
+        s.add_point_light((-1, 1, -1), (1, 1, 1))
+        return s, params(max_reflection_level=0, glossy_ray_count=1), 256, 256, \
+            "cube.obj 256x256, primary rays, depth 0, 1 point light"
+    if name == "C2":
+        s.preset(PRESETS["Monkey"], dd)
+        return s, params(max_reflection_level=1, glossy_ray_count=1), 1024, 1024, \
+            "monkey-rotated.obj 1024x1024, Phong + hard shadows, depth 1"
+    if name in ("C3", "C4"):
+        u, v = dragon_uv or (DRAGON_U, DRAGON_V)
+        s.load_obj(dragon_proxy_path(u, v), normalize=True)
+        if name == "C3":
+            s.add_point_light((-1, 1, -1), (1, 1, 1))
+            return s, params(max_reflection_level=4, glossy_ray_count=1), 1920, 1080, \
+                f"dragon-proxy ({2 * u * v} tris) 1920x1080, hard shadows + mirror depth 4"
+        s.add_spherical_light((-1, 1, -1), 0.1, (1, 1, 1))
+        return s, params(max_reflection_level=0, sphere_light_ray_count=64, glossy_ray_count=1), 1920, 1080, \
+            f"dragon-proxy ({2 * u * v} tris) 1920x1080, spherical light 64 samples"
+    if name == "C5":
+        s.preset(PRESETS["CornellBox"], dd)  # meshes + glass sphere + point light
+        s.clear_lights()
+        third = float(np.float32(1.0) / np.float32(3.0))
+        for dx in (0.0, -0.3, 0.3):
+            pos = (float(np.float32(-0.1) + np.float32(dx)), 0.63, -0.1)
+            s.add_plane_light(pos, (0.15, -0.05, 0.0), (0.0, 0.0, 0.2), (third, third, third))
+        return s, params(max_reflection_level=8, plane_light_1D_ray_count=8, glossy_ray_count=1), 3840, 2160, \
+            "CornellBox-Mirror-Rotated 3840x2160, depth 8, 3 plane lights x 64 samples"
+    raise ValueError(name)
