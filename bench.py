@@ -1,0 +1,203 @@
+"""bench.py -- Mrays/s of the MI355X ray tracer on BASELINE.json's 1920x1080 workload.
+
+Workload (config.workload): C3 = dragon proxy (800 000 triangles), 1920x1080,
+one point light, hard shadows + mirror recursion depth 4 (BASELINE.json configs[2]).  One step
+renders one full frame: every rank renders its interleaved 8-row bands on its own GPU, the bands
+are gathered over RCCL (torch.distributed "nccl") and rank 0 un-permutes them into the
+Screen::m_textureData layout.  Inputs (scene, BVH) are resident in HBM before timing starts.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3] [--no-cpu-baseline]
+
+Prints ONE JSON line on rank 0.  `value` = rays (intersect() calls) of all ranks / max-rank time.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "raytracer-group27_amd"))
+
+import numpy as np  # noqa: E402
+
+METRIC = "Mrays/s (primary+shadow+secondary) at 1920×1080; fraction of HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+BAND_ROWS = 8
+
+
+def algorithmic_bytes(st, pixels):
+    """64 B per BVH2 node visit, 64 B per triangle record, 68 B per shaded hit
+    (3 normals + material), 12 B per pixel written."""
+    return 64 * st.node_visits + 64 * st.tri_tests + 68 * st.hits + 12 * pixels
+
+
+def cpu_baseline(config, budget_s=12.0, seed=12345):
+    """Reference algorithm (oracle/ref_cpu.cpp: brute-force primary/secondary rays, depth-4 BVH for
+    shadow rays) timed single-threaded on a fixed pseudo-random pixel sample of the same frame."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O
+    import rt_amd as R
+
+    scene, prm, W, H, _ = R.build_config(config)
+    O.set_threads(1)
+    orc = O.Oracle(scene)
+    rng = np.random.default_rng(seed)
+    order = rng.permutation(W * H)
+    rays = 0
+    npx = 0
+    t0 = time.perf_counter()
+    chunk = 4
+    while time.perf_counter() - t0 < budget_s and npx < len(order):
+        sel = order[npx:npx + chunk]
+        xy = np.stack([sel % W, sel // W], axis=1)
+        _, r = orc.render_pixels(prm, W, H, xy)
+        rays += int(r.sum())
+        npx += len(sel)
+    dt = time.perf_counter() - t0
+    return {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "port",
+            "sample": f"{npx} pseudo-random pixels (seed {seed}) of {config} {W}x{H}, {rays} rays in {dt:.1f} s, "
+                      f"OMP_NUM_THREADS=1, host CPU: {_cpu_model()}"}
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def load_pmc(config):
+    """HBM bytes per render launch from a committed rocprofv3 --pmc run (tools/profile.sh), or None."""
+    p = os.path.join(REPO, "profiles", "pmc_latest.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        if d.get("config") == config:
+            return d.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="C3")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import rt_amd as R
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    scene, prm, W, H, desc = R.build_config(args.config)
+    cam = R.camera_from_trackball(aspect=R.aspect_of(W, H))
+    t_up = time.perf_counter()
+    ctx = R.Context(scene, device=local)
+    upload_s = time.perf_counter() - t_up
+
+    nbands = (H + BAND_ROWS - 1) // BAND_ROWS
+    max_local = (nbands + world - 1) // world
+    local_buf = torch.zeros(max_local * BAND_ROWS * W * 3, dtype=torch.float32, device=dev)
+    gathered = torch.zeros(world * local_buf.numel(), dtype=torch.float32, device=dev) if world > 1 else local_buf
+    image = torch.zeros(W * H * 3, dtype=torch.float32, device=dev)
+
+    def step():
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        st = ctx.render_device(cam, prm, W, H, BAND_ROWS, rank, world, local_buf.data_ptr(), stream)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, local_buf)
+        if rank == 0:
+            R.check(R.lib().rt_unpermute_bands_device(W, H, BAND_ROWS, world, R.C.c_void_p(gathered.data_ptr()),
+                                                      R.C.c_void_p(image.data_ptr()), R.C.c_void_p(stream)))
+        return st
+
+    # counting pass (same kernel, COUNT=true) for the algorithmic-byte roofline numerator
+    R.set_counting(True)
+    cst = step()
+    R.set_counting(False)
+    for _ in range(args.warmup):
+        step()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    barrier()
+    t0 = time.perf_counter()
+    rays = 0
+    kms = []
+    for _ in range(args.steps):
+        st = step()
+        rays += st.rays
+        kms.append(st.kernel_ms)
+    barrier()
+    elapsed = time.perf_counter() - t0
+
+    t = torch.tensor([elapsed, float(rays), float(np.mean(kms)), float(cst.node_visits), float(cst.tri_tests),
+                      float(cst.hits), float(cst.rays)], dtype=torch.float64, device=dev)
+    if world > 1:
+        allv = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(allv, t)
+        allv = torch.stack(allv).cpu().numpy()
+    else:
+        allv = t.cpu().numpy()[None, :]
+    max_elapsed = float(allv[:, 0].max())
+    total_rays = float(allv[:, 1].sum())
+
+    if rank == 0:
+        # roofline of the dominant kernel (render_kernel) on rank 0's launches
+        pixels0 = int(((nbands - rank + world - 1) // world) * BAND_ROWS * W)
+        bytes0 = algorithmic_bytes(cst, min(pixels0, W * H))
+        avg_ms = float(np.mean(kms))
+        achieved = bytes0 / (avg_ms * 1e-3) / 1e9
+        pmc = load_pmc(args.config)
+        line = {
+            "metric": METRIC,
+            "value": total_rays / max_elapsed / 1e6,
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": max_elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (deterministic 800k-triangle torus-knot stand-in for the missing data/dragon.obj)",
+            "config": {"workload": f"{args.config}: {desc}", "resolution": f"{W}x{H}", "rays_per_frame":
+                       int(total_rays / args.steps), "band_rows": BAND_ROWS, "partition": f"{world} GPU band split",
+                       "scene_upload_s": round(upload_s, 3)},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": (float(pmc) if pmc is not None else None),
+                         "kernel": "render_kernel<false>", "kernel_avg_ms": avg_ms,
+                         "algorithmic_bytes_per_launch": int(bytes0)},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args.config, budget_s=args.cpu_budget)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
