@@ -232,7 +232,32 @@ __device__ bool traverse(const DevScene& S, v3 o, v3 d, v3 nd, float t_init, flo
     int sp = 0;
     int node = 0;
     bool found = false;
-    if (S.ntri > 0) {
+    // The reference measures t along normalize(dir) but places the test point at o + dir*t
+    // (src/ray_tracing.cpp:71,111), so for a non-unit direction the accepted point lies off the
+    // triangle and no bounding volume can find it: such rays (only reachable through
+    // rt_intersect / rt_shade; every ray the renderer makes is unit length) test every record.
+    const float dd = dot(d, d);
+    if (!(fabsf(dd - 1.0f) <= 4e-6f)) {
+        for (int r = 0; r < S.ntri; ++r) {
+            const float4* tp = S.tri + r * 4;
+            const float4 r0 = tp[0], r1 = tp[1], r2 = tp[2], r3 = tp[3];
+            if (COUNT) cnt.tris++;
+            float t;
+            if (!tri_test(r0, r1, r2, r3, o, d, nd, t)) continue;
+            const int key = REF ? __float_as_int(r3.z) : __float_as_int(r3.y);
+            if (ANY) {
+                if (!(t <= thr)) continue;
+            } else {
+                if (!(t < best.t || (t == best.t && key < best.key))) continue;
+            }
+            if (REF && !leaf_reachable(S, __float_as_int(r3.w), o, nd, mask)) continue;
+            best.t = t;
+            best.key = key;
+            best.rec = r;
+            found = true;
+            if (ANY) return true;
+        }
+    } else if (S.ntri > 0) {
         for (;;) {
             const float4* np = S.nodes + node * 4;
             const float4 a = np[0];

@@ -232,7 +232,7 @@ class Scene:
         pos = np.ctypeslib.as_array(d.positions, shape=(T * 9,)).reshape(T, 3, 3).copy() if T else np.zeros((0, 3, 3), np.float32)
         nrm = np.ctypeslib.as_array(d.normals, shape=(T * 9,)).reshape(T, 3, 3).copy() if T else np.zeros((0, 3, 3), np.float32)
         mesh = np.ctypeslib.as_array(d.mesh_index, shape=(T,)).copy() if T else np.zeros((0,), np.int32)
-        mats = [d.materials[i] for i in range(d.num_meshes)]
+        mats = [rt_material.from_buffer_copy(d.materials[i]) for i in range(d.num_meshes)]
         return pos, nrm, mesh, mats
 
 
@@ -340,6 +340,37 @@ class Context:
 
 def set_counting(on):
     check(lib().rt_set_counting(int(on)))
+
+
+# --------------------------------------------------------------------------------------------
+# Multi-GPU band partition (rt_render_device / rt_unpermute_bands_device contract)
+# --------------------------------------------------------------------------------------------
+def band_rows_of(H, band_rows, rank, count):
+    """Image rows (reference y, 0 = bottom) a rank renders, in its dense output order."""
+    nbands = (H + band_rows - 1) // band_rows
+    rows = []
+    for gb in range(rank, nbands, count):
+        rows.extend(range(gb * band_rows, min((gb + 1) * band_rows, H)))
+    return rows
+
+
+def local_band_elems(W, H, band_rows, count):
+    """Floats in one rank's (padded) band buffer: max_local_bands * band_rows * W * 3."""
+    nbands = (H + band_rows - 1) // band_rows
+    return ((nbands + count - 1) // count) * band_rows * W * 3
+
+
+def unpermute_host(gathered, W, H, band_rows, count):
+    """Host statement of unpermute_kernel: gathered [count][max_local][band_rows][W][3] ->
+    Screen::m_textureData order (row H-1-y first, src/screen.cpp:32-38)."""
+    nbands = (H + band_rows - 1) // band_rows
+    max_local = (nbands + count - 1) // count
+    g = np.asarray(gathered, np.float32).reshape(count, max_local, band_rows, W, 3)
+    out = np.zeros((H, W, 3), np.float32)
+    for y in range(H):
+        gb, r = divmod(y, band_rows)
+        out[H - 1 - y] = g[gb % count, gb // count, r]
+    return out.reshape(-1)
 
 
 # --------------------------------------------------------------------------------------------

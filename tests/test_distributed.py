@@ -1,0 +1,76 @@
+"""World-size-2 gloo rehearsal of the multi-GPU path (bench.py): each rank renders its interleaved
+8-row bands, the padded band buffers are all-gathered and rank 0 un-permutes them.  The bands are
+rendered here by the CPU oracle (no GPU in this container); the GPU test
+tests/test_gpu_parity.py::test_band_split_bit_identical runs the same layout through the HIP kernel."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, W, H, band_rows, out_path):
+    sys.path.insert(0, os.path.join(REPO, "raytracer-group27_amd"))
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O
+    import rt_amd as R
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    O.set_threads(1)
+    scene, prm, _, _, _ = R.build_config("C2")
+    orc = O.Oracle(scene)
+    rows = R.band_rows_of(H, band_rows, rank, world)
+    xy = np.array([(x, y) for y in rows for x in range(W)], np.int32)
+    rgb, rays = orc.render_pixels(prm, W, H, xy)
+    local = np.zeros(R.local_band_elems(W, H, band_rows, world), np.float32)
+    local[:rgb.size] = rgb.reshape(-1)
+    t = torch.from_numpy(local)
+    gathered = torch.zeros(world * t.numel(), dtype=torch.float32)
+    dist.all_gather_into_tensor(gathered, t)
+    total = torch.tensor([float(rays.sum())], dtype=torch.float64)
+    dist.all_reduce(total)
+    if rank == 0:
+        img = R.unpermute_host(gathered.numpy(), W, H, band_rows, world)
+        np.savez(out_path, img=img, rays=total.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,W,H,band_rows", [(2, 24, 20, 8), (2, 17, 9, 4), (3, 16, 33, 8)])
+def test_band_split_gather_matches_single_render(tmp_path, world, W, H, band_rows):
+    sys.path.insert(0, os.path.join(REPO, "raytracer-group27_amd"))
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O
+    import rt_amd as R
+
+    out = str(tmp_path / "img.npz")
+    mp.start_processes(_worker, args=(world, _free_port(), W, H, band_rows, out), nprocs=world, join=True,
+                       start_method="spawn")
+    z = np.load(out)
+    scene, prm, _, _, _ = R.build_config("C2")
+    ref, rays = O.Oracle(scene).render(prm, W, H)
+    assert z["img"].tobytes() == ref.tobytes()
+    assert int(z["rays"][0]) == rays
+
+
+def test_band_rows_cover_image_once():
+    sys.path.insert(0, os.path.join(REPO, "raytracer-group27_amd"))
+    import rt_amd as R
+
+    for H, br, n in [(1080, 8, 8), (1080, 8, 3), (2160, 8, 7), (5, 8, 2)]:
+        rows = [r for k in range(n) for r in R.band_rows_of(H, br, k, n)]
+        assert sorted(rows) == list(range(H))

@@ -1,0 +1,181 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle and the golden vectors.
+
+Tolerance: every pixel within 1e-5 absolute of the oracle (BASELINE.json north_star); geometry
+(t, hit points, normals, primitive ids, ray counts) must be bit-identical.  Full-size configs are
+checked on sampled pixels plus size-independent properties (determinism, band-split invariance)."""
+import os
+
+import numpy as np
+import pytest
+
+from golden_cases import IMAGES, PRESET_IMAGES, apply
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+
+
+@pytest.fixture(scope="module")
+def ctxs(R):
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    cache = {}
+
+    def get(cfg, uv=None):
+        key = (cfg, uv)
+        if key not in cache:
+            scene, prm, W, H, _ = R.build_config(cfg, dragon_uv=uv)
+            cache[key] = (scene, R.Context(scene), prm, W, H)
+        return cache[key]
+
+    yield get
+    for v in cache.values():
+        v[1].close()
+
+
+def golden(golden_dir):
+    z = np.load(f"{golden_dir}/images.npz")
+    out = {}
+    for k in z.files:
+        name, field = k.split("__")
+        out.setdefault(name, {})[field] = z[k]
+    return out
+
+
+@pytest.mark.parametrize("case", IMAGES, ids=[c[0] for c in IMAGES])
+def test_golden_images(R, ctxs, golden_dir, case):
+    name, cfg, W, H, uv, over = case
+    g = golden(golden_dir)[name]
+    scene, ctx, prm, _, _ = ctxs(cfg, uv)
+    prm = apply(R.rt_params.from_buffer_copy(prm), over)
+    cam = R.camera_from_trackball(aspect=R.aspect_of(W, H))
+    img, st = ctx.render(cam, prm, W, H)
+    assert st.rays == int(g["rays"])
+    assert float(np.max(np.abs(img - g["img"]))) <= TOL
+
+
+@pytest.mark.parametrize("case", PRESET_IMAGES, ids=[c[0] for c in PRESET_IMAGES])
+def test_golden_presets(R, golden_dir, case):
+    name, preset, W, H, over = case
+    g = golden(golden_dir)[name]
+    scene = R.Scene().preset(R.PRESETS[preset], R.data_dir())
+    ctx = R.Context(scene)
+    prm = apply(R.params(), over)
+    img, st = ctx.render(R.camera_from_trackball(aspect=R.aspect_of(W, H)), prm, W, H)
+    ctx.close()
+    assert st.rays == int(g["rays"])
+    assert float(np.max(np.abs(img - g["img"]))) <= TOL
+
+
+@pytest.mark.parametrize("cfg", ["C1", "C2", "C5"])
+@pytest.mark.parametrize("use_bvh", [0, 1])
+def test_intersect_kats_bit_exact(R, ctxs, golden_dir, cfg, use_bvh):
+    z = np.load(f"{golden_dir}/kats.npz")
+    _, ctx, _, _, _ = ctxs(cfg)
+    hits = ctx.intersect(z[f"{cfg}__rays"], use_bvh)
+    ref = z[f"{cfg}_bvh{use_bvh}__hits"]
+    assert np.array_equal(hits["hit"], ref["hit"])
+    assert hits["t"].tobytes() == ref["t"].tobytes()
+    h = ref["hit"] == 1
+    for f in ("normal", "hit_point", "material_index", "prim_id", "is_triangle"):
+        assert hits[f][h].tobytes() == ref[f][h].tobytes(), f
+
+
+@pytest.mark.parametrize("cfg", ["C2", "C5"])
+def test_shade_matches_oracle(R, O, ctxs, golden_dir, cfg):
+    """getFinalColor(level 0) on arbitrary rays (KAT rays: unit and non-unit directions)."""
+    z = np.load(f"{golden_dir}/kats.npz")
+    scene, ctx, prm, _, _ = ctxs(cfg)
+    rays = z[f"{cfg}__rays"][:600]
+    rgb, cnt = ctx.shade(rays, prm)
+    ref, rcnt = O.Oracle(scene).shade(rays, prm)
+    assert np.array_equal(cnt, rcnt)
+    assert float(np.max(np.abs(rgb - ref))) <= TOL
+
+
+def test_full_frame_c1_c2(R, O, ctxs):
+    for cfg in ("C1", "C2"):
+        scene, ctx, prm, W, H = ctxs(cfg)
+        img, st = ctx.render(R.camera_from_trackball(aspect=R.aspect_of(W, H)), prm, W, H)
+        ref, rays = O.Oracle(scene).render(prm, W, H)
+        assert st.rays == rays, cfg
+        assert float(np.max(np.abs(img - ref))) <= TOL, cfg
+
+
+@pytest.mark.parametrize("cfg", ["C3", "C4", "C5"])
+def test_full_size_sampled_pixels(R, O, ctxs, cfg):
+    """Full BASELINE resolution on the GPU; a fixed pixel sample (half of them on geometry)
+    re-rendered by the oracle."""
+    scene, ctx, prm, W, H = ctxs(cfg)
+    img, st = ctx.render(R.camera_from_trackball(aspect=R.aspect_of(W, H)), prm, W, H)
+    assert np.isfinite(img).all()
+    view = img.reshape(H, W, 3)[::-1]  # [y][x] in reference y order
+    rng = np.random.default_rng(12345)
+    lit = np.argwhere(view.max(axis=2) > 0)
+    n = 24 if cfg != "C5" else 12
+    pick = lit[rng.choice(len(lit), size=min(n, len(lit)), replace=False)]
+    rand = np.stack([rng.integers(0, H, n), rng.integers(0, W, n)], axis=1)
+    yx = np.concatenate([pick, rand])
+    xy = yx[:, ::-1].astype(np.int32)
+    ref, _ = O.Oracle(scene).render_pixels(prm, W, H, xy)
+    got = view[yx[:, 0], yx[:, 1]]
+    assert float(np.max(np.abs(got - ref))) <= TOL
+
+
+@pytest.mark.parametrize("cfg,uv", [("C3", (200, 80)), ("C5", None)])
+def test_band_split_bit_identical(R, ctxs, cfg, uv):
+    """The multi-GPU layout (interleaved 8-row bands per rank + un-permute) reproduces the
+    single-GPU frame bit for bit, and a re-render is deterministic."""
+    import ctypes
+
+    import torch
+
+    scene, ctx, prm, _, _ = ctxs(cfg, uv)
+    W, H = 200, 123
+    cam = R.camera_from_trackball(aspect=R.aspect_of(W, H))
+    full, st = ctx.render(cam, prm, W, H)
+    again, _ = ctx.render(cam, prm, W, H)
+    assert full.tobytes() == again.tobytes()
+    for count in (2, 3, 8):
+        n = R.local_band_elems(W, H, 8, count)
+        gathered = torch.zeros(count * n, dtype=torch.float32, device="cuda")
+        rays = 0
+        for rank in range(count):
+            part = gathered[rank * n:(rank + 1) * n]
+            s = ctx.render_device(cam, prm, W, H, 8, rank, count, part.data_ptr(), None)
+            rays += s.rays
+        torch.cuda.synchronize()
+        img = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda")
+        R.check(R.lib().rt_unpermute_bands_device(W, H, 8, count, ctypes.c_void_p(gathered.data_ptr()),
+                                                  ctypes.c_void_p(img.data_ptr()), None))
+        torch.cuda.synchronize()
+        assert img.cpu().numpy().tobytes() == full.tobytes()
+        host = R.unpermute_host(gathered.cpu().numpy(), W, H, 8, count)
+        assert host.tobytes() == full.tobytes()
+        assert rays == st.rays
+
+
+def test_device_math_is_ieee(R, ctxs):
+    _, ctx, _, _, _ = ctxs("C1")
+    rng = np.random.default_rng(3)
+    x = np.concatenate([rng.uniform(1e-6, 10, 20000), rng.uniform(-1, 1, 20000)]).astype(np.float32)
+    x[x == 0] = 1.0
+    y = rng.uniform(-4, 250, len(x)).astype(np.float32)
+    out = ctx.selftest_math(x, y)
+    with np.errstate(all="ignore"):
+        pos = x > 0
+        assert out[pos, 0].tobytes() == np.sqrt(x[pos]).tobytes()  # correctly rounded sqrt
+        assert out[:, 1].tobytes() == (np.float32(1) / x).tobytes()  # correctly rounded division
+        assert out[:, 2].tobytes() == (x / y).tobytes()
+        ref = np.power(x[pos].astype(np.float64), y[pos].astype(np.float64)).astype(np.float32)
+        got = out[pos, 3]
+        fin = np.isfinite(ref) & (ref != 0)
+        ulp = np.abs(got[fin].view(np.int32).astype(np.int64) - ref[fin].view(np.int32).astype(np.int64))
+        assert ulp.max() <= 2  # powf feeds colours only (calcColor specular)
+
+
+def test_invalid_params_fail_loudly(R, ctxs):
+    _, ctx, prm, _, _ = ctxs("C1")
+    bad = R.params(max_reflection_level=99, glossy_ray_count=1)
+    with pytest.raises(R.RtError, match="max_reflection_level"):
+        ctx.render(R.camera_from_trackball(), bad, 8, 8)
