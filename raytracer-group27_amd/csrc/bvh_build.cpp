@@ -191,6 +191,8 @@ struct Box {
     }
 };
 
+constexpr int kMaxDepth = 36;
+
 struct Bvh2Builder {
     std::vector<Box> pbox;
     std::vector<v3> cent;
@@ -222,7 +224,13 @@ struct Bvh2Builder {
         const float cext = axis == 0 ? ext.x : (axis == 1 ? ext.y : ext.z);
         auto cval = [&](int p) { return axis == 0 ? cent[p].x : (axis == 1 ? cent[p].y : cent[p].z); };
         int mid = -1;
-        if (cext > 0.0f && depth < 40) {
+        // depth guard: median splits halve the range, so switching to them once
+        // depth + ceil(log2(n / max_leaf)) reaches kMaxDepth bounds the tree depth (and the
+        // traversal stack, RT_STACK_SIZE) by kMaxDepth + 1.
+        int need = 0;
+        while ((max_leaf << need) < n) ++need;
+        const bool sah_ok = depth + need < kMaxDepth;
+        if (cext > 0.0f && sah_ok) {
             constexpr int NB = 32;
             Box bb[NB];
             int bc[NB] = {0};

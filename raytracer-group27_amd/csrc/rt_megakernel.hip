@@ -1,0 +1,714 @@
+// rt_megakernel.hip -- persistent ray-state-machine megakernel (included by rt_runtime.hip after
+// rt_kernels.hip, whose device helpers it reuses).
+//
+// Why: the recursive reference (getFinalColor -> lights -> cansee -> intersect) compiled as nested
+// inlined calls gives ~5 traversal instances, 256 VGPRs and one wave per SIMD, and a wave is held
+// by its slowest pixel.  Here every lane is a small state machine whose only expensive step is
+// ONE shared traversal: in each iteration every busy lane traces whatever query its state needs
+// (camera ray, mirror/refracted ray, or a shadow segment), then advances its state until it needs
+// the next query.  A lane that finishes its pixel takes the next one from a global counter
+// (wave-aggregated atomic), so no lane idles while work remains.
+//
+// The arithmetic of every step is exactly the reference's (same helpers as rt_kernels.hip); only
+// the schedule differs.  Reference map: pixel/sample loop src/main.cpp:344-395, getFinalColor
+// :129-301, lights src/shadow.cpp:106-321, cansee src/shadow.cpp:32-69.
+
+namespace rt {
+
+enum QType { Q_PATH = 0, Q_SHADOW = 1 };
+enum LType { L_POINT = 0, L_SPHERE = 1, L_SPOT = 2, L_PLANE = 3, L_DONE = 4 };
+
+struct Lane {
+    // job
+    int job;     // -1: idle
+    int sample;  // sub-sample index (AA / getPixelRays)
+    int nsamples;
+    int px, py, out_row;  // pixel, row inside the local band buffer
+    v3 pacc;
+    // query
+    v3 qo, qd;
+    float qt;  // initial ray.t
+    int qtype;
+    // path
+    int level;
+    v3 cur_d;  // direction of the ray that produced the current shading point
+    // shading point
+    v3 hp, nN, nR, refl;
+    int mat;  // >= 0 mesh material, < 0: sphere -(s+1)
+    v3 color;
+    // light loop
+    int lt, li, ls;
+    float a0, a1, a2, a3;  // per-light accumulators
+    v3 u0, u1;             // perp | (px, py)
+    // cansee
+    v3 so, sd;
+    float sdist, sI;
+};
+
+__device__ __forceinline__ DMat load_mat(const DevScene& S, int m) {
+    if (m >= 0) return S.mats[m];
+    return S.sph[-m - 1].m;
+}
+
+// Traversal with run-time mode flags: one instance serves every query type.
+template <bool COUNT>
+__device__ __forceinline__ bool trace_query(const DevScene& S, v3 o, v3 d, float t_init, float thr, bool REF, bool ANY,
+                                            Best& best, int* stk, Cnt& cnt) {
+    const v3 nd = normalize(d);
+    best.t = t_init;
+    best.key = -1;
+    best.rec = RT_NO_HIT;
+    RefMask mask{0u, 0u};
+    float tcull = ANY ? thr : t_init;
+    bool found = false;
+    const float dd = dot(d, d);
+    const bool unit = fabsf(dd - 1.0f) <= 4e-6f;
+    const v3 inv = safe_inv(d);
+    int sp = 0;
+    int node = 0;
+    // non-unit directions: exhaustive (see traverse() in rt_kernels.hip); unit: BVH2
+    int brute_r = 0;
+    const int brute_n = unit ? 0 : S.ntri;
+    bool done = (S.ntri == 0);
+    while (!done) {
+        int first = 0, count = 0;
+        if (!unit) {
+            first = brute_r;
+            count = min(64, brute_n - brute_r);
+            brute_r += count;
+            done = brute_r >= brute_n;
+        } else {
+            const float4* np = S.nodes + node * 4;
+            const float4 a = np[0];
+            const float4 b = np[1];
+            const float4 c = np[2];
+            const float4 e = np[3];
+            const int c0 = __float_as_int(e.x), c1 = __float_as_int(e.y);
+            const int n0 = __float_as_int(e.z), n1 = __float_as_int(e.w);
+            if (COUNT) cnt.nodes++;
+            float tn0 = 0.0f, tn1 = 0.0f;
+            bool h0 = (c0 >= 0) && box_hit(a.x, a.y, a.z, a.w, b.x, b.y, o, inv, tcull, tn0);
+            bool h1 = (c1 >= 0) && box_hit(b.z, b.w, c.x, c.y, c.z, c.w, o, inv, tcull, tn1);
+            const bool l0 = h0 && n0 > 0, l1 = h1 && n1 > 0;
+            h0 = h0 && n0 == 0;
+            h1 = h1 && n1 == 0;
+            // at most two leaf ranges per node: test them below, then descend
+            if (l0 && l1) {
+                // adjacent ranges are not guaranteed; test both in turn
+                for (int r = c0; r < c0 + n0; ++r) {
+                    const float4* tp = S.tri + r * 4;
+                    const float4 r0 = tp[0], r1 = tp[1], r2 = tp[2], r3 = tp[3];
+                    if (COUNT) cnt.tris++;
+                    float t;
+                    if (!tri_test(r0, r1, r2, r3, o, d, nd, t)) continue;
+                    const int key = REF ? __float_as_int(r3.z) : __float_as_int(r3.y);
+                    if (ANY ? !(t <= thr) : !(t < best.t || (t == best.t && key < best.key))) continue;
+                    if (REF && !leaf_reachable(S, __float_as_int(r3.w), o, nd, mask)) continue;
+                    best.t = t;
+                    best.key = key;
+                    best.rec = r;
+                    found = true;
+                    if (!ANY) tcull = t;
+                }
+                if (ANY && found) break;
+                first = c1;
+                count = n1;
+            } else if (l0) {
+                first = c0;
+                count = n0;
+            } else if (l1) {
+                first = c1;
+                count = n1;
+            }
+            h0 = h0 && tn0 <= tcull;
+            h1 = h1 && tn1 <= tcull;
+            if (h0 && h1) {
+                const bool near0 = tn0 <= tn1;
+                stk[sp * RT_WAVE] = near0 ? c1 : c0;
+                ++sp;
+                node = near0 ? c0 : c1;
+            } else if (h0) {
+                node = c0;
+            } else if (h1) {
+                node = c1;
+            } else if (sp == 0) {
+                done = true;
+            } else {
+                --sp;
+                node = stk[sp * RT_WAVE];
+            }
+        }
+        for (int r = first; r < first + count; ++r) {
+            const float4* tp = S.tri + r * 4;
+            const float4 r0 = tp[0], r1 = tp[1], r2 = tp[2], r3 = tp[3];
+            if (COUNT) cnt.tris++;
+            float t;
+            if (!tri_test(r0, r1, r2, r3, o, d, nd, t)) continue;
+            const int key = REF ? __float_as_int(r3.z) : __float_as_int(r3.y);
+            if (ANY ? !(t <= thr) : !(t < best.t || (t == best.t && key < best.key))) continue;
+            if (REF && !leaf_reachable(S, __float_as_int(r3.w), o, nd, mask)) continue;
+            best.t = t;
+            best.key = key;
+            best.rec = r;
+            found = true;
+            if (!ANY) tcull = t;
+        }
+        if (ANY && found) break;
+    }
+    if (!(ANY && found)) {
+        for (int s = 0; s < S.nsph; ++s) {
+            const DSph sp_ = S.sph[s];
+            float t;
+            if (!sphere_test(sp_, o, d, t)) continue;
+            const int key = REF ? sp_.key_bvh : S.ntri + s;
+            if (ANY ? !(t <= thr) : !(t < best.t || (t == best.t && key < best.key))) continue;
+            if (REF && !leaf_reachable(S, sp_.leaf, o, nd, mask)) continue;
+            best.t = t;
+            best.key = key;
+            best.rec = -s - 1;
+            found = true;
+            if (ANY) break;
+        }
+    }
+    return found;
+}
+
+// ---- light loop -----------------------------------------------------------------------------
+// Starts cansee(hp, target) (src/shadow.cpp:32-40).  Returns true if a shadow query is needed;
+// otherwise the loop condition `distance > SHADOW_ERROR_OFFSET` failed and cansee returns true.
+__device__ __forceinline__ bool start_cansee(Lane& L, v3 target) {
+    v3 d = target - L.hp;
+    L.sdist = length(d);
+    d = normalize(d);
+    L.so = L.hp + 0.0005f * d;
+    L.sd = d;
+    L.sI = 1.0f;
+    if (L.sdist > 0.0005f) {
+        L.qo = L.so;
+        L.qd = L.sd;
+        L.qt = FLT_MAX;
+        L.qtype = Q_SHADOW;
+        return true;
+    }
+    return false;
+}
+
+__device__ __forceinline__ void light_cos(const Lane& L, v3 lp, float& cosL, float& cosS) {
+    const v3 ldir = normalize(lp - L.hp);
+    cosL = fabsf(dot(L.nN, ldir));
+    const float d2 = dot(L.nR, ldir);
+    cosS = (0.0f < d2) ? d2 : 0.0f;
+}
+
+// Sample target of the current light sample; false when the current light is finished (or
+// skipped) and the caller must move on.
+__device__ __forceinline__ v3 sphere_perp(const Lane& L, v3 lp, float radius) {
+    v3 dd = normalize(lp - L.hp);
+    v3 notd = dd;
+    if (dd.x != 0.0f) {
+        notd.y = -dd.x;
+        notd.x = dd.y;
+    } else {
+        notd.y = -dd.z;
+        notd.z = dd.y;
+    }
+    return normalize(cross(dd, notd)) * radius;
+}
+
+// Advance the light loop until a shadow query is needed (true) or all lights are done (false).
+// `vis` carries the result of the cansee that just finished (valid when have_result).
+__device__ bool advance_lights(const KParams& P, Lane& L, bool have_result, bool vis) {
+    const DevScene& S = P.S;
+    for (;;) {
+        if (L.lt == L_POINT) {
+            if (have_result) {
+                have_result = false;
+                if (vis) {
+                    const rt_point_light pl = S.pl[L.li];
+                    float cosL, cosS;
+                    light_cos(L, ld3(pl.position), cosL, cosS);
+                    L.color += calc_color(ld3(pl.color), L.sI, cosL, cosS, load_mat(S, L.mat));
+                }
+                L.li++;
+            }
+            if (L.li >= S.npl) {
+                L.lt = L_SPHERE;
+                L.li = 0;
+                L.ls = -1;
+                continue;
+            }
+            if (start_cansee(L, ld3(S.pl[L.li].position))) return true;
+            have_result = true;
+            vis = true;
+            continue;
+        }
+        if (L.lt == L_SPHERE) {
+            if (L.li >= S.nsl) {
+                L.lt = L_SPOT;
+                L.li = 0;
+                continue;
+            }
+            const rt_spherical_light sl = S.sl[L.li];
+            const v3 lp = ld3(sl.position);
+            if (have_result) {
+                have_result = false;
+                if (L.ls == -1) {
+                    L.a0 = L.sI;  // intensitySum is the centre sample's intensity (mutated even if blocked)
+                    L.a1 = vis ? 1.0f : 0.0f;
+                    L.u0 = sphere_perp(L, lp, sl.radius);
+                    L.ls = 0;
+                } else {
+                    if (vis) {
+                        L.a1 += 1.0f;
+                        L.a0 += L.sI;
+                    }
+                    const int j = L.ls % P.sl_m;
+                    if (j == P.sl_m - 1) {  // end of a spoke: perp = rotate * perp
+                        const m3 rot = rodrigues(P.sl_sin, P.sl_1mcos, normalize(lp - L.hp));
+                        L.u0 = mul(rot, L.u0);
+                    }
+                    L.ls++;
+                }
+            }
+            if (L.ls >= P.sl_m * P.sl_n) {
+                if (L.a1 > 0.0f) {
+                    float cosL, cosS;
+                    light_cos(L, lp, cosL, cosS);
+                    L.color += calc_color(ld3(sl.color), L.a0 / (float)P.sl_count, cosL, cosS, load_mat(S, L.mat));
+                }
+                L.li++;
+                L.ls = -1;
+                continue;
+            }
+            v3 target = lp;
+            if (L.ls >= 0) {
+                const int m = P.sl_m;
+                const int j = L.ls % m;
+                target = lp + ((float)(m - j) / (float)m) * L.u0;
+            }
+            if (start_cansee(L, target)) return true;
+            have_result = true;
+            vis = true;
+            continue;
+        }
+        if (L.lt == L_SPOT) {
+            if (have_result) {
+                have_result = false;
+                if (vis) {
+                    const DSpot sp = S.spot[L.li];
+                    float cosL, cosS;
+                    light_cos(L, ld3(sp.pos), cosL, cosS);
+                    L.color += calc_color(ld3(sp.color), L.sI, cosL, cosS, load_mat(S, L.mat));
+                }
+                L.li++;
+            }
+            if (L.li >= S.nspot) {
+                L.lt = L_PLANE;
+                L.li = 0;
+                L.ls = -1;
+                continue;
+            }
+            const DSpot sp = S.spot[L.li];
+            const v3 lp = ld3(sp.pos);
+            if (!(dot(normalize(ld3(sp.dir)), normalize(L.hp - lp)) > sp.cos_angle)) {
+                L.li++;
+                continue;
+            }
+            if (start_cansee(L, lp)) return true;
+            have_result = true;
+            vis = true;
+            continue;
+        }
+        if (L.lt == L_PLANE) {
+            if (L.li >= S.nplane) {
+                L.lt = L_DONE;
+                return false;
+            }
+            const rt_plane_light pl = S.plane[L.li];
+            const int k = P.plane_k;
+            const v3 w = ld3(pl.width), h = ld3(pl.height), lpos = ld3(pl.position);
+            const v3 normal = normalize(cross(w, h));
+            if (L.ls == -1) {
+                // hit, hitCount, maxCos, intensitySum; px, py (src/shadow.cpp:259-270)
+                L.a0 = 0.0f;
+                L.a1 = 0.0f;
+                L.a2 = 0.0f;
+                L.a3 = 0.0f;
+                L.u1 = lpos;
+                L.u0 = lpos;
+                if (dot(normalize(L.hp - (lpos + 0.5f * (w + h))), normal) > 0.0f) {
+                    L.ls = 0;
+                } else {
+                    L.ls = k * k;  // not in front of the light: no samples
+                }
+            } else if (have_result) {
+                have_result = false;
+                if (vis) {
+                    const v3 px = L.u0;
+                    L.a3 += L.sI;
+                    const float dn = dot(normalize(L.hp - px), normal);
+                    L.a0 += ((dn < 0.0f) ? 0.0f : dn) / length(L.hp - px);
+                    L.a1 += 1.0f;
+                    const float c2 = dot(L.nR, normalize(px - L.hp));
+                    L.a2 = (L.a2 < c2) ? c2 : L.a2;
+                }
+                const v3 dx = (1.0f / (float)(k - 1)) * w;
+                L.u0 = L.u0 + dx;
+                const int j = L.ls % k;
+                if (j == k - 1) {
+                    const v3 dy = (1.0f / (float)(k - 1)) * h;
+                    L.u1 = L.u1 + dy;
+                    L.u0 = L.u1;
+                }
+                L.ls++;
+            }
+            if (L.ls >= k * k) {
+                if (L.a0 > 0.0f) {
+                    const float li = (L.a3 / (float)(int)L.a1) * L.a0 / (float)(k * k);
+                    L.color += calc_color(ld3(pl.color), li, 1.0f, L.a2, load_mat(S, L.mat));
+                }
+                L.li++;
+                L.ls = -1;
+                continue;
+            }
+            if (start_cansee(L, L.u0)) return true;
+            have_result = true;
+            vis = true;
+            continue;
+        }
+        return false;  // L_DONE
+    }
+}
+
+// ---- recursion tree ------------------------------------------------------------------------
+// After the direct light of the shading point at L.level: descend (returns true with the
+// child ray queued) or fold the finished subtree into its ancestors.  Returns false when the
+// level-0 colour is complete (in `out`).
+__device__ bool finish_node(const KParams& P, Lane& L, Frame* fr, bool hit, v3& out) {
+    v3 child = L.color;
+    if (!hit) child = v3{0.0f, 0.0f, 0.0f};
+    if (hit && L.level < P.max_level) {
+        const DMat m = load_mat(P.S, L.mat);
+        if (m.transp == 1.0f) {
+            if (m.ks[0] > 0.0f || m.ks[1] > 0.0f || m.ks[2] > 0.0f) {
+                Frame& f = fr[L.level];
+                f.color = L.color;
+                f.w = v3{m.ks[0], m.ks[1], m.ks[2]};
+                f.mode = FR_MIRROR;
+                f.flag = (m.shin != 0.0f);
+                L.qo = L.hp + 0.01f * L.refl;
+                L.qd = L.refl;
+                L.qt = FLT_MAX;
+                L.qtype = Q_PATH;
+                L.level++;
+                return true;
+            }
+        } else {
+            const v3 l = normalize(L.cur_d);
+            const v3 n = L.nN;
+            const float r = P.refr;
+            const float c = fabsf(dot(l, n));
+            v3 refr = r * l + (r * c - sqrtf(1.0f - r * r * (1.0f - c * c))) * n;
+            refr = normalize(refr);
+            const float R0 = m.transp;
+            const float reflC = (float)((double)R0 + (double)(1.0f - R0) * pow((double)(1.0f - c), 5.0));
+            const float refrC = 1.0f - reflC;
+            Frame& f = fr[L.level];
+            f.color = L.color;
+            f.w = v3{reflC, refrC, 0.0f};
+            f.o2 = L.hp + 0.01f * refr;
+            f.d2 = refr;
+            f.mode = FR_TRANS_A;
+            f.flag = (r * r * (1.0f - c * c) <= 1.0f);
+            L.qo = L.hp + 0.01f * L.refl;
+            L.qd = L.refl;
+            L.qt = FLT_MAX;
+            L.qtype = Q_PATH;
+            L.level++;
+            return true;
+        }
+    }
+    while (L.level > 0) {
+        L.level--;
+        Frame& f = fr[L.level];
+        if (f.mode == FR_MIRROR) {
+            const v3 rc = v3{0.0f, 0.0f, 0.0f} + f.w * child;
+            const v3 add = f.flag ? (f.w * rc) / (float)P.glossy_n : f.w * rc;
+            child = f.color + add;
+        } else if (f.mode == FR_TRANS_A) {
+            f.color = f.color + f.w.x * child;
+            if (f.flag) {
+                f.mode = FR_TRANS_B;
+                L.qo = f.o2;
+                L.qd = f.d2;
+                L.qt = FLT_MAX;
+                L.qtype = Q_PATH;
+                L.level++;
+                return true;
+            }
+            child = f.color;
+        } else {
+            child = f.color + f.w.y * child;
+        }
+    }
+    out = child;
+    return false;
+}
+
+// ---- jobs ----------------------------------------------------------------------------------
+struct JobSrc {
+    int mode;  // 0: pixels of the band layout, 1: explicit rays (rt_shade)
+    int njobs;
+    const rt_ray* rays;
+    float* rgb;                    // mode 1 output [n][3]
+    unsigned long long* ray_counts;  // mode 1 per-ray counts
+    int* counter;                  // global job counter (zeroed per launch)
+};
+
+// queue the camera ray of the lane's current sample (src/main.cpp:350-386)
+__device__ __forceinline__ void queue_camera(const KParams& P, Lane& L) {
+    const float ndx = (float)L.px / (float)P.W * 2.0f - 1.0f;
+    const float ndy = (float)L.py / (float)P.H * 2.0f - 1.0f;
+    float sx = ndx, sy = ndy;
+    if (P.aa) {
+        const int s = L.sample;
+        sx = (s == 0 || s == 2) ? ndx - P.aa_offx : ndx + P.aa_offx;
+        sy = (s < 2) ? ndy + P.aa_offy : ndy - P.aa_offy;
+    } else if (P.multi) {
+        const int per_q = ((P.ms_moves + 1) / 2) * ((P.ms_moves + 1) / 2);
+        const int q = L.sample / per_q;
+        const int r = L.sample % per_q;
+        const int nyv = (P.ms_moves + 1) / 2;
+        const int xx = 1 + 2 * (r / nyv);
+        const int yy = 1 + 2 * (r % nyv);
+        const float qx = (q == 0 || q == 2) ? -1.0f : 1.0f;
+        const float qy = (q < 2) ? 1.0f : -1.0f;
+        sx = ndx + (P.ms_offx * qx * (float)xx);
+        sy = ndy + (P.ms_offy * qy * (float)yy);
+    }
+    v3 o, d;
+    gen_ray(P, sx, sy, o, d);
+    L.qo = o;
+    L.qd = d;
+    L.qt = FLT_MAX;
+    L.qtype = Q_PATH;
+    L.level = 0;
+}
+
+// Map a job index to its pixel (8x8 tiles inside the rank's bands).  False if outside the image.
+__device__ __forceinline__ bool job_pixel(const KParams& P, int job, Lane& L) {
+    const int tiles_x = (P.W + 7) / 8;
+    const int tiles_y_band = (P.band_rows + 7) / 8;
+    const int tile = job >> 6;
+    const int lane = job & 63;
+    const int tx = tile % tiles_x;
+    const int rest = tile / tiles_x;
+    const int ty = rest % tiles_y_band;
+    const int lb = rest / tiles_y_band;
+    const int gb = lb * P.band_count + P.band_rank;
+    const int row_in_band = ty * 8 + (lane >> 3);
+    L.px = tx * 8 + (lane & 7);
+    L.py = gb * P.band_rows + row_in_band;
+    L.out_row = lb * P.band_rows + row_in_band;
+    return (L.px < P.W) && (row_in_band < P.band_rows) && (L.py < P.H) && (lb < P.n_local_bands);
+}
+
+template <bool COUNT, int WPE>
+__global__ __launch_bounds__(64, WPE) void persistent_kernel(KParams P, JobSrc J) {
+    __shared__ int stack_lds[RT_STACK_SIZE * RT_WAVE];
+    __shared__ int s_base;
+    const int lane_id = threadIdx.x;
+    int* stk = stack_lds + lane_id;
+    const DevScene& S = P.S;
+    Frame fr[RT_MAX_DEPTH];
+    Lane L;
+    L.job = -1;
+    Cnt cnt{0u, 0u, 0u, 0u};
+    Cnt job_cnt{0u, 0u, 0u, 0u};  // per-job ray count (rt_shade)
+    bool need_trace = false;
+    for (;;) {
+        // ---- refill idle lanes (one atomic per wave) ----
+        const bool idle = (L.job < 0);
+        const unsigned long long want = __ballot(idle);
+        if (want) {
+            if (lane_id == __ffsll((long long)want) - 1) s_base = atomicAdd(J.counter, __popcll(want));
+            __builtin_amdgcn_wave_barrier();
+            __syncthreads();
+            const int base = s_base;
+            if (idle) {
+                const int myrank = __popcll(want & ((1ull << lane_id) - 1ull));
+                const int job = base + myrank;
+                if (job < J.njobs) {
+                    L.job = job;
+                    L.sample = 0;
+                    L.pacc = v3{0.0f, 0.0f, 0.0f};
+                    job_cnt.rays = 0u;
+                    if (J.mode == 0) {
+                        if (!job_pixel(P, job, L)) {
+                            L.job = -1;  // padding pixel: nothing to do, fetch again next round
+                        } else {
+                            L.nsamples = P.aa ? 4 : (P.multi ? P.sample_size : 1);
+                            queue_camera(P, L);
+                            need_trace = true;
+                        }
+                    } else {
+                        const rt_ray r = J.rays[job];
+                        L.nsamples = 1;
+                        L.qo = v3{r.origin[0], r.origin[1], r.origin[2]};
+                        L.qd = v3{r.direction[0], r.direction[1], r.direction[2]};
+                        L.qt = r.t;
+                        L.qtype = Q_PATH;
+                        L.level = 0;
+                        need_trace = true;
+                    }
+                } else {
+                    L.job = -2;  // no more work for this lane
+                }
+            }
+            __syncthreads();
+        }
+        const bool busy = need_trace && L.job >= 0;
+        if (!__any(busy)) {
+            if (!__any(L.job == -1)) break;  // every lane exhausted
+            continue;
+        }
+        // ---- the one traversal ----
+        Best b;
+        bool hit = false;
+        if (busy) {
+            cnt.rays++;
+            job_cnt.rays++;
+            const bool shadow = (L.qtype == Q_SHADOW);
+            const bool ref = shadow || P.use_bvh;
+            const bool any = shadow && S.all_opaque;
+            const float thr = L.sdist - 2.0f * 0.0005f;
+            hit = trace_query<COUNT>(S, L.qo, L.qd, L.qt, thr, ref, any, b, stk, cnt);
+        }
+        if (!busy) continue;
+        // ---- advance the state machine until the next query ----
+        need_trace = false;
+        if (L.qtype == Q_SHADOW) {
+            bool vis;
+            bool again = false;
+            if (S.all_opaque) {
+                vis = !hit;
+            } else if (!hit || b.t > L.sdist - 2.0f * 0.0005f) {
+                vis = true;
+            } else {
+                const Surf s = surface(S, L.qo, L.qd, b);
+                if (s.m.transp != 1.0f) {
+                    L.sdist -= b.t;
+                    L.so = s.p + 0.0005f * L.sd;
+                    const float c = fabsf(dot(L.sd, s.n));
+                    const float R0 = s.m.transp;
+                    L.sI = (float)((double)L.sI *
+                                   (1.0 - ((double)R0 + (double)(1.0f - R0) * pow((double)(1.0f - c), 5.0))));
+                    if (L.sdist > 0.0005f) {
+                        L.qo = L.so;
+                        L.qd = L.sd;
+                        L.qt = FLT_MAX;
+                        again = true;
+                    }
+                    vis = true;  // loop exit without an opaque blocker
+                } else {
+                    vis = false;
+                }
+            }
+            if (again) {
+                need_trace = true;
+                continue;
+            }
+            if (advance_lights(P, L, true, vis)) {
+                need_trace = true;
+                continue;
+            }
+        } else {
+            // a getFinalColor node (src/main.cpp:131-190)
+            L.cur_d = L.qd;
+            if (!hit) {
+                L.color = v3{0.0f, 0.0f, 0.0f};
+            } else {
+                if (COUNT) cnt.hits++;
+                const Surf s = surface(S, L.qo, L.qd, b);
+                L.hp = s.p;
+                L.nN = normalize(s.n);
+                L.refl = reflect(normalize(L.qd), L.nN);
+                L.nR = normalize(L.refl);
+                L.mat = (b.rec >= 0) ? s.mesh : b.rec;
+                L.color = v3{0.0f, 0.0f, 0.0f};
+                L.lt = L_POINT;
+                L.li = 0;
+                L.ls = -1;
+                if (advance_lights(P, L, false, false)) {
+                    need_trace = true;
+                    continue;
+                }
+            }
+            // fall through to finish with hit/miss
+            v3 out;
+            if (finish_node(P, L, fr, hit, out)) {
+                need_trace = true;
+                continue;
+            }
+            // level-0 colour complete
+            if (J.mode == 0) {
+                if (P.aa || P.multi) L.pacc += out;
+                else L.pacc = out;
+                L.sample++;
+                if (L.sample < L.nsamples) {
+                    queue_camera(P, L);
+                    need_trace = true;
+                    continue;
+                }
+                v3 col = L.pacc;
+                if (P.aa) col = L.pacc * 0.25f;
+                else if (P.multi) col = L.pacc * (float)(1.0f / (float)P.sample_size);
+                float* dst = P.out + ((size_t)L.out_row * P.W + L.px) * 3;
+                dst[0] = col.x;
+                dst[1] = col.y;
+                dst[2] = col.z;
+            } else {
+                J.rgb[L.job * 3 + 0] = out.x;
+                J.rgb[L.job * 3 + 1] = out.y;
+                J.rgb[L.job * 3 + 2] = out.z;
+                J.ray_counts[L.job] = job_cnt.rays;
+            }
+            L.job = -1;
+            continue;
+        }
+        // shadow path finished every light: the node is complete
+        {
+            v3 out;
+            if (finish_node(P, L, fr, true, out)) {
+                need_trace = true;
+                continue;
+            }
+            if (J.mode == 0) {
+                if (P.aa || P.multi) L.pacc += out;
+                else L.pacc = out;
+                L.sample++;
+                if (L.sample < L.nsamples) {
+                    queue_camera(P, L);
+                    need_trace = true;
+                    continue;
+                }
+                v3 col = L.pacc;
+                if (P.aa) col = L.pacc * 0.25f;
+                else if (P.multi) col = L.pacc * (float)(1.0f / (float)P.sample_size);
+                float* dst = P.out + ((size_t)L.out_row * P.W + L.px) * 3;
+                dst[0] = col.x;
+                dst[1] = col.y;
+                dst[2] = col.z;
+            } else {
+                J.rgb[L.job * 3 + 0] = out.x;
+                J.rgb[L.job * 3 + 1] = out.y;
+                J.rgb[L.job * 3 + 2] = out.z;
+                J.ray_counts[L.job] = job_cnt.rays;
+            }
+            L.job = -1;
+        }
+    }
+    flush_counters<COUNT>(P, cnt);
+}
+
+}  // namespace rt

@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -14,6 +15,7 @@
 #include "bvh_build.h"
 #include "rt_internal.h"
 #include "rt_kernels.hip"
+#include "rt_megakernel.hip"
 
 using namespace rt;
 
@@ -32,7 +34,46 @@ struct rt_ctx {
     int ref_nodes = 0, ref_levels = 0;
     int bvh_depth = 0;
     bool glossy_material = false;  // opaque, ks > 0, shininess != 0 (glossy_ray_count > 1 would call rand())
+    int persistent_blocks[5] = {0, 0, 0, 0, 0};  // resident 64-lane blocks per WPE variant
 };
+
+// waves per SIMD the persistent kernel is compiled for (register cap); RT_WPE overrides for A/B runs
+static int wpe() {
+    const char* w = std::getenv("RT_WPE");
+    const int v = w ? std::atoi(w) : 2;
+    return (v >= 1 && v <= 4) ? v : 2;
+}
+
+template <bool COUNT>
+static void launch_persistent(int grid, hipStream_t st, const KParams& K, const JobSrc& J) {
+    switch (wpe()) {
+        case 1: hipLaunchKernelGGL((persistent_kernel<COUNT, 1>), dim3(grid), dim3(64), 0, st, K, J); break;
+        case 3: hipLaunchKernelGGL((persistent_kernel<COUNT, 3>), dim3(grid), dim3(64), 0, st, K, J); break;
+        case 4: hipLaunchKernelGGL((persistent_kernel<COUNT, 4>), dim3(grid), dim3(64), 0, st, K, J); break;
+        default: hipLaunchKernelGGL((persistent_kernel<COUNT, 2>), dim3(grid), dim3(64), 0, st, K, J); break;
+    }
+}
+
+static int persistent_grid(rt_ctx* c) {
+    if (c->persistent_blocks[wpe()] > 0) return c->persistent_blocks[wpe()];
+    int cus = 0, per_cu = 0;
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
+    hipError_t e = hipErrorInvalidValue;
+    switch (wpe()) {
+        case 1: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_kernel<false, 1>, 64, 0); break;
+        case 3: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_kernel<false, 3>, 64, 0); break;
+        case 4: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_kernel<false, 4>, 64, 0); break;
+        default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_kernel<false, 2>, 64, 0); break;
+    }
+    if (e != hipSuccess || per_cu <= 0) per_cu = 8;
+    c->persistent_blocks[wpe()] = std::max(1, cus) * per_cu;
+    return c->persistent_blocks[wpe()];
+}
+
+static bool use_tile_kernel() {
+    const char* k = std::getenv("RT_KERNEL");
+    return k && std::strcmp(k, "tile") == 0;
+}
 
 #define HIP_TRY(expr)                                                                           \
     do {                                                                                        \
@@ -352,10 +393,22 @@ static int launch_render(rt_ctx* c, KParams& K, hipStream_t st, int count_mode, 
     HIP_TRY(hipMemsetAsync(c->d_stats, 0, 8 * sizeof(unsigned long long), st));
     if (blocks > 0) {
         HIP_TRY(hipEventRecord(c->ev0, st));
-        if (count_mode)
-            hipLaunchKernelGGL(render_kernel<true>, dim3((unsigned)blocks), dim3(64), 0, st, K);
-        else
-            hipLaunchKernelGGL(render_kernel<false>, dim3((unsigned)blocks), dim3(64), 0, st, K);
+        if (use_tile_kernel()) {
+            if (count_mode)
+                hipLaunchKernelGGL(render_kernel<true>, dim3((unsigned)blocks), dim3(64), 0, st, K);
+            else
+                hipLaunchKernelGGL(render_kernel<false>, dim3((unsigned)blocks), dim3(64), 0, st, K);
+        } else {
+            JobSrc J{};
+            J.mode = 0;
+            J.njobs = (int)(blocks * 64);
+            J.counter = reinterpret_cast<int*>(c->d_stats + 6);
+            const int grid = (int)std::min<long long>(blocks, persistent_grid(c));
+            if (count_mode)
+                launch_persistent<true>(grid, st, K, J);
+            else
+                launch_persistent<false>(grid, st, K, J);
+        }
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(c->ev1, st));
     }
@@ -491,7 +544,20 @@ extern "C" int rt_shade(rt_ctx* c, const rt_ray* rays, int n, const rt_params* p
     HIP_TRY(hipMalloc(&d_c, sizeof(float) * 3 * n));
     HIP_TRY(hipMalloc(&d_n, sizeof(unsigned long long) * n));
     hipMemcpy(d_r, rays, sizeof(rt_ray) * n, hipMemcpyHostToDevice);
-    hipLaunchKernelGGL(shade_kernel, dim3((n + 63) / 64), dim3(64), 0, c->stream, K, d_r, n, d_c, d_n);
+    if (use_tile_kernel()) {
+        hipLaunchKernelGGL(shade_kernel, dim3((n + 63) / 64), dim3(64), 0, c->stream, K, d_r, n, d_c, d_n);
+    } else {
+        JobSrc J{};
+        J.mode = 1;
+        J.njobs = n;
+        J.rays = d_r;
+        J.rgb = d_c;
+        J.ray_counts = d_n;
+        J.counter = reinterpret_cast<int*>(c->d_stats + 6);
+        hipMemsetAsync(c->d_stats, 0, 8 * sizeof(unsigned long long), c->stream);
+        const int grid = std::min((n + 63) / 64, persistent_grid(c));
+        launch_persistent<false>(grid, c->stream, K, J);
+    }
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e == hipSuccess) e = hipMemcpy(rgb, d_c, sizeof(float) * 3 * n, hipMemcpyDeviceToHost);
