@@ -208,6 +208,8 @@ int rt_shade(rt_ctx* ctx, const rt_ray* rays, int n, const rt_params* params, fl
 
 /* Counting build of the same kernel (node visits, triangle records, hits) for roofline accounting. */
 int rt_set_counting(int on);
+/* Debug counters of the last counting launch (per-query node-visit histogram, maxima). */
+int rt_debug_counters(rt_ctx* ctx, uint64_t* out, int n);
 
 /* Introspection for tests / roofline accounting. */
 int rt_ctx_info(rt_ctx* ctx, int* num_nodes, int* num_tri_records, int* ref_bvh_nodes,

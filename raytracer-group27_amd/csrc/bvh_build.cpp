@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstring>
 #include <queue>
 #include <stdexcept>
 #include <utility>
@@ -355,6 +356,143 @@ Bvh2 build_bvh2(const float* pos, int ntri, float eps, int max_leaf) {
     out.nodes = std::move(b.nodes);
     out.order = std::move(b.idx);
     out.max_depth = b.max_depth;
+    return out;
+}
+
+// ---------------------------------------------------------------------------------------------
+// BVH8 collapse + conservative 16-bit quantisation
+// ---------------------------------------------------------------------------------------------
+namespace {
+struct Child2 {
+    float lo[3], hi[3];
+    int child, count;  // Bvh2 descriptor: count > 0 leaf range in b2.order, else inner node index
+};
+
+static float area_of(const Child2& c) {
+    const float dx = c.hi[0] - c.lo[0], dy = c.hi[1] - c.lo[1], dz = c.hi[2] - c.lo[2];
+    return 2.0f * (dx * dy + dy * dz + dz * dx);
+}
+
+static void children_of(const Bvh2& b2, int node, std::vector<Child2>& out) {
+    const Bvh2Node& n = b2.nodes[node];
+    for (int k = 0; k < 2; ++k) {
+        if (n.child[k] < 0 && n.count[k] == 0) continue;  // empty slot
+        Child2 c;
+        const float* lo = k == 0 ? n.lo0 : n.lo1;
+        const float* hi = k == 0 ? n.hi0 : n.hi1;
+        for (int a = 0; a < 3; ++a) {
+            c.lo[a] = lo[a];
+            c.hi[a] = hi[a];
+        }
+        c.child = n.child[k];
+        c.count = n.count[k];
+        out.push_back(c);
+    }
+}
+
+static float decode(float origin, int e, uint32_t q) {
+    const float scale = std::ldexp(1.0f, e);
+    return origin + (float)q * scale;  // same two IEEE ops as the device decode
+}
+}  // namespace
+
+Bvh8 build_bvh8(const Bvh2& b2, int width) {
+    Bvh8 out;
+    if (width < 2 || width > 8) throw std::runtime_error("BVH8 width must be 2..8");
+    if (b2.nodes.empty()) return out;
+    struct Item {
+        int node2;  // Bvh2 inner node whose subtree this BVH8 node covers
+        int slot;   // BVH8 node index
+        int depth;
+    };
+    std::vector<Item> queue;
+    queue.push_back({0, 0, 1});
+    out.nodes.assign(32, 0u);
+    size_t head = 0;
+    while (head < queue.size()) {
+        const Item it = queue[head++];
+        out.max_depth = std::max(out.max_depth, it.depth);
+        std::vector<Child2> ch;
+        children_of(b2, it.node2, ch);
+        // greedy collapse: open the inner child with the largest surface area until `width` children
+        for (;;) {
+            if ((int)ch.size() >= width) break;
+            int best = -1;
+            float best_a = -1.0f;
+            for (size_t i = 0; i < ch.size(); ++i)
+                if (ch[i].count == 0 && area_of(ch[i]) > best_a) {
+                    best_a = area_of(ch[i]);
+                    best = (int)i;
+                }
+            if (best < 0) break;
+            std::vector<Child2> sub;
+            children_of(b2, ch[best].child, sub);
+            if ((int)(ch.size() - 1 + sub.size()) > width) break;
+            ch.erase(ch.begin() + best);
+            ch.insert(ch.end(), sub.begin(), sub.end());
+        }
+        uint32_t* w = out.nodes.data() + (size_t)it.slot * 32;
+        // node box = union of the children
+        float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+        for (const Child2& c : ch)
+            for (int a = 0; a < 3; ++a) {
+                lo[a] = std::min(lo[a], c.lo[a]);
+                hi[a] = std::max(hi[a], c.hi[a]);
+            }
+        int e[3];
+        for (int a = 0; a < 3; ++a) {
+            std::memcpy(&w[a], &lo[a], 4);
+            const double ext = (double)hi[a] - (double)lo[a];
+            int ex = -126;
+            while (ex < 127 && std::ldexp(65000.0, ex) < ext) ++ex;
+            // the device forms 2^e * (1/d) with |1/d| <= 1e20: keep it finite
+            if (ex > 40) throw std::runtime_error("BVH8: scene extent too large to quantise");
+            e[a] = ex;
+        }
+        w[3] = (uint32_t)(e[0] + 127) | ((uint32_t)(e[1] + 127) << 8) | ((uint32_t)(e[2] + 127) << 16);
+        uint32_t imask = 0, lmask = 0, counts = 0;
+        const int child_base = (int)(out.nodes.size() / 32);
+        const int tri_base = (int)out.order.size();
+        w[4] = (uint32_t)child_base;
+        w[5] = (uint32_t)tri_base;
+        int n_inner = 0;
+        uint16_t q[6][8];
+        for (int s = 0; s < 8; ++s)
+            for (int k = 0; k < 6; ++k) q[k][s] = (k < 3) ? 65535 : 0;  // empty: inverted box
+        for (size_t s = 0; s < ch.size(); ++s) {
+            const Child2& c = ch[s];
+            for (int a = 0; a < 3; ++a) {
+                const float scale = std::ldexp(1.0f, e[a]);
+                long ql = (long)std::floor(((double)c.lo[a] - (double)lo[a]) / scale);
+                long qh = (long)std::ceil(((double)c.hi[a] - (double)lo[a]) / scale);
+                ql = std::max(0L, std::min(65535L, ql));
+                qh = std::max(0L, std::min(65535L, qh));
+                while (ql > 0 && decode(lo[a], e[a], (uint32_t)ql) > c.lo[a]) --ql;
+                while (qh < 65535 && decode(lo[a], e[a], (uint32_t)qh) < c.hi[a]) ++qh;
+                if (decode(lo[a], e[a], (uint32_t)ql) > c.lo[a] || decode(lo[a], e[a], (uint32_t)qh) < c.hi[a])
+                    throw std::runtime_error("BVH8 quantisation is not conservative");
+                q[a][s] = (uint16_t)ql;
+                q[3 + a][s] = (uint16_t)qh;
+            }
+            if (c.count > 0) {
+                lmask |= 1u << s;
+                counts |= (uint32_t)c.count << (4 * s);
+                for (int r = c.child; r < c.child + c.count; ++r) out.order.push_back(b2.order[r]);
+            } else {
+                imask |= 1u << s;
+                n_inner++;
+            }
+        }
+        w[6] = imask | (lmask << 8);
+        w[7] = counts;
+        for (int k = 0; k < 6; ++k)
+            for (int s = 0; s < 8; s += 2) w[8 + k * 4 + s / 2] = (uint32_t)q[k][s] | ((uint32_t)q[k][s + 1] << 16);
+        // allocate the inner children contiguously, in slot order
+        out.nodes.resize(out.nodes.size() + (size_t)n_inner * 32, 0u);
+        int rank = 0;
+        for (size_t s = 0; s < ch.size(); ++s)
+            if (ch[s].count == 0) queue.push_back({ch[s].child, child_base + rank++, it.depth + 1});
+    }
     return out;
 }
 

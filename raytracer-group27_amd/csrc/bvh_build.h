@@ -55,4 +55,22 @@ struct Bvh2 {
 
 Bvh2 build_bvh2(const float* positions, int ntri, float eps, int max_leaf = 4);
 
+// Wide BVH collapsed from a Bvh2 (greedy: open the child with the largest area until `width`
+// children, width <= 8; slots past `width` stay empty),
+// 128-B nodes with 16-bit child boxes quantised conservatively against the node origin:
+//   dword 0-2 origin xyz (f32) | 3: (ex+127) | (ey+127)<<8 | (ez+127)<<16 (scale = 2^e)
+//   4: child_base (first internal child node; internal children are contiguous in slot order)
+//   5: tri_base (first record of the node's leaf children, contiguous in slot order)
+//   6: internal-child mask | leaf-child mask << 8
+//   7: per-slot triangle count, 4 bits per slot (0 for internal / empty slots)
+//   8-31: q_lo_x[8] q_lo_y[8] q_lo_z[8] q_hi_x[8] q_hi_y[8] q_hi_z[8] as uint16
+// decoded bound = origin + float(q) * 2^e, verified on the host to contain the child box.
+struct Bvh8 {
+    std::vector<uint32_t> nodes;  // 32 dwords per node
+    std::vector<int> order;       // record i -> scene triangle index
+    int max_depth = 0;
+};
+
+Bvh8 build_bvh8(const Bvh2& b2, int width = 8);
+
 }  // namespace rt

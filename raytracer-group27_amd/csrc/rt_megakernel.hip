@@ -173,6 +173,160 @@ __device__ __forceinline__ bool trace_query(const DevScene& S, v3 o, v3 d, float
     return found;
 }
 
+// 8-wide traversal over the quantised BVH8 (bvh_build.h).  The stack holds node groups
+// (node << 8 | mask of inner children not yet visited), one per tree level, so it is bounded by
+// the tree depth; a popped group's boxes are re-tested against the current best t and the
+// nearest survivor is visited next.  Every candidate is judged with the same reference
+// arithmetic and (t, key) order as trace_query.
+template <bool COUNT>
+__device__ __forceinline__ bool test_records(const DevScene& S, int first, int count, v3 o, v3 d, v3 nd, float thr,
+                                             bool REF, bool ANY, Best& best, RefMask& mask, float& tcull,
+                                             bool& found, Cnt& cnt) {
+    for (int r = first; r < first + count; ++r) {
+        const float4* tp = S.tri + r * 4;
+        const float4 r0 = tp[0], r1 = tp[1], r2 = tp[2], r3 = tp[3];
+        if (COUNT) cnt.tris++;
+        float t;
+        if (!tri_test(r0, r1, r2, r3, o, d, nd, t)) continue;
+        const int key = REF ? __float_as_int(r3.z) : __float_as_int(r3.y);
+        if (ANY ? !(t <= thr) : !(t < best.t || (t == best.t && key < best.key))) continue;
+        if (REF && !leaf_reachable(S, __float_as_int(r3.w), o, nd, mask)) continue;
+        best.t = t;
+        best.key = key;
+        best.rec = r;
+        found = true;
+        if (ANY) return true;
+        tcull = t;
+    }
+    return false;
+}
+
+__device__ __forceinline__ float pow2f(uint32_t biased) { return __int_as_float((int)(biased << 23)); }
+
+template <bool COUNT, int NW>
+__device__ __forceinline__ bool trace_query8(const DevScene& S, v3 o, v3 d, float t_init, float thr, bool REF,
+                                             bool ANY, Best& best, int* stk, Cnt& cnt) {
+    const v3 nd = normalize(d);
+    best.t = t_init;
+    best.key = -1;
+    best.rec = RT_NO_HIT;
+    RefMask mask{0u, 0u};
+    float tcull = ANY ? thr : t_init;
+    bool found = false;
+    const float dd = dot(d, d);
+    if (!(fabsf(dd - 1.0f) <= 4e-6f)) {
+        // non-unit direction: exhaustive (see traverse() in rt_kernels.hip)
+        if (test_records<COUNT>(S, 0, S.ntri, o, d, nd, thr, REF, ANY, best, mask, tcull, found, cnt)) return true;
+    } else if (S.ntri > 0) {
+        const v3 inv = safe_inv(d);
+        const float4* nodes = S.nodes;
+        int sp = 0;
+        uint32_t cur = 0xFFu;  // node 0, every slot
+        // software pipeline: the next node's 128 B are requested before this node's leaf
+        // triangles are tested, so the two memory latencies overlap
+        float4 g0 = nodes[0], g1 = nodes[1], g2 = nodes[2], g3 = nodes[3];
+        float4 g4 = nodes[4], g5 = nodes[5], g6 = nodes[6], g7 = nodes[7];
+        for (;;) {
+            const uint32_t node = cur >> 8;
+            const float4 f0 = g0, f1 = g1, qlx = g2, qly = g3, qlz = g4, qhx = g5, qhy = g6, qhz = g7;
+            if (COUNT) cnt.nodes++;
+            const uint32_t w3 = __float_as_uint(f0.w);
+            const uint32_t imask = __float_as_uint(f1.z) & 0xFFu;
+            const uint32_t lmask = (__float_as_uint(f1.z) >> 8) & 0xFFu;
+            const uint32_t counts = __float_as_uint(f1.w);
+            const uint32_t child_base = __float_as_uint(f1.x);
+            const uint32_t tri_base = __float_as_uint(f1.y);
+            // slab distances straight from the 16-bit offsets: t = q * (2^e * inv) + (origin - o) * inv.
+            // The two rounded products differ from the decoded-box form by a few ulps of |t|, the
+            // same order as the decoded form's own error, and far inside the eps inflation.
+            const float bx = pow2f(w3 & 0xFFu) * inv.x, by = pow2f((w3 >> 8) & 0xFFu) * inv.y,
+                        bz = pow2f((w3 >> 16) & 0xFFu) * inv.z;
+            const float ax = (f0.x - o.x) * inv.x, ay = (f0.y - o.y) * inv.y, az = (f0.z - o.z) * inv.z;
+            const uint32_t m = (cur & 0xFFu) & (imask | lmask);
+            // box tests; the nearest inner child is chosen here so no per-slot distances stay live.
+            uint32_t hits = 0;
+            float tbest = FLT_MAX;
+            int sbest = -1;
+#pragma unroll
+            for (int s = 0; s < NW; ++s) {
+                if (m & (1u << s)) {
+                    const int wi = s >> 1, sh = (s & 1) * 16;
+                    auto q = [&](const float4& f) {
+                        const uint32_t wv = __float_as_uint(wi == 0 ? f.x : wi == 1 ? f.y : wi == 2 ? f.z : f.w);
+                        return (float)((wv >> sh) & 0xFFFFu);
+                    };
+                    const float tlx = fmaf(q(qlx), bx, ax), thx = fmaf(q(qhx), bx, ax);
+                    const float tly = fmaf(q(qly), by, ay), thy = fmaf(q(qhy), by, ay);
+                    const float tlz = fmaf(q(qlz), bz, az), thz = fmaf(q(qhz), bz, az);
+                    const float t0 = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fminf(tlz, thz));
+                    const float t1 = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fmaxf(tlz, thz));
+                    if (t0 <= t1 && t1 >= 0.0f && t0 <= tcull) {
+                        hits |= 1u << s;
+                        if ((imask & (1u << s)) && (t0 < tbest || sbest < 0)) {
+                            tbest = t0;
+                            sbest = s;
+                        }
+                    }
+                }
+            }
+            // next node (decided before the leaf tests; a child or group that the leaf hits put
+            // out of reach is culled when it is tested): the nearest inner child, the rest kept as
+            // a group (node << 8 | slots) on the stack, else the top group
+            const uint32_t ih = hits & imask;
+            bool more = true;
+            if (ih) {
+                const uint32_t rest = ih & ~(1u << sbest);
+                if (rest) {
+                    stk[sp * RT_WAVE] = (int)((node << 8) | rest);
+                    ++sp;
+                }
+                const uint32_t rank = __popc(imask & ((1u << sbest) - 1u));
+                cur = ((child_base + rank) << 8) | 0xFFu;
+            } else if (sp > 0) {
+                --sp;
+                cur = (uint32_t)stk[sp * RT_WAVE];
+            } else {
+                more = false;
+            }
+            if (more) {
+                const float4* np = nodes + (size_t)(cur >> 8) * 8;
+                g0 = np[0], g1 = np[1], g2 = np[2], g3 = np[3];
+                g4 = np[4], g5 = np[5], g6 = np[6], g7 = np[7];
+            }
+            // leaf children: records tri_base + (counts of lower leaf slots), in slot order
+            uint32_t lh = hits & lmask;
+            while (lh) {
+                const int s = __ffs(lh) - 1;
+                lh &= lh - 1u;
+                const uint32_t below = s ? (counts & ((1u << (4 * s)) - 1u)) : 0u;
+                uint32_t nib = (below & 0x0F0F0F0Fu) + ((below >> 4) & 0x0F0F0F0Fu);
+                nib = (nib * 0x01010101u) >> 24;
+                const int cnt_s = (int)((counts >> (4 * s)) & 15u);
+                if (test_records<COUNT>(S, (int)(tri_base + nib), cnt_s, o, d, nd, thr, REF, ANY, best, mask, tcull,
+                                        found, cnt))
+                    return true;
+            }
+            if (!more) break;
+        }
+    }
+    if (!(ANY && found)) {
+        for (int s = 0; s < S.nsph; ++s) {
+            const DSph sp_ = S.sph[s];
+            float t;
+            if (!sphere_test(sp_, o, d, t)) continue;
+            const int key = REF ? sp_.key_bvh : S.ntri + s;
+            if (ANY ? !(t <= thr) : !(t < best.t || (t == best.t && key < best.key))) continue;
+            if (REF && !leaf_reachable(S, sp_.leaf, o, nd, mask)) continue;
+            best.t = t;
+            best.key = key;
+            best.rec = -s - 1;
+            found = true;
+            if (ANY) break;
+        }
+    }
+    return found;
+}
+
 // ---- light loop -----------------------------------------------------------------------------
 // Starts cansee(hp, target) (src/shadow.cpp:32-40).  Returns true if a shadow query is needed;
 // otherwise the loop condition `distance > SHADOW_ERROR_OFFSET` failed and cansee returns true.
@@ -513,7 +667,7 @@ __device__ __forceinline__ bool job_pixel(const KParams& P, int job, Lane& L) {
     return (L.px < P.W) && (row_in_band < P.band_rows) && (L.py < P.H) && (lb < P.n_local_bands);
 }
 
-template <bool COUNT, int WPE>
+template <bool COUNT, int WPE, int BW>
 __global__ __launch_bounds__(64, WPE) void persistent_kernel(KParams P, JobSrc J) {
     __shared__ int stack_lds[RT_STACK_SIZE * RT_WAVE];
     __shared__ int s_base;
@@ -582,11 +736,18 @@ __global__ __launch_bounds__(64, WPE) void persistent_kernel(KParams P, JobSrc J
             const bool ref = shadow || P.use_bvh;
             const bool any = shadow && S.all_opaque;
             const float thr = L.sdist - 2.0f * 0.0005f;
-            hit = trace_query<COUNT>(S, L.qo, L.qd, L.qt, thr, ref, any, b, stk, cnt);
+            if (BW > 2)
+                hit = trace_query8<COUNT, BW>(S, L.qo, L.qd, L.qt, thr, ref, any, b, stk, cnt);
+            else
+                hit = trace_query<COUNT>(S, L.qo, L.qd, L.qt, thr, ref, any, b, stk, cnt);
         }
         if (!busy) continue;
         // ---- advance the state machine until the next query ----
+        // Each step below has exactly one call site (advance_lights, finish_node, pixel output):
+        // inlined twice, the light loop and the recursion fold pushed the kernel past 256 VGPRs.
         need_trace = false;
+        bool run_lights = false, lights_have = false, lights_vis = false;
+        bool node_hit = true;
         if (L.qtype == Q_SHADOW) {
             bool vis;
             bool again = false;
@@ -618,15 +779,15 @@ __global__ __launch_bounds__(64, WPE) void persistent_kernel(KParams P, JobSrc J
                 need_trace = true;
                 continue;
             }
-            if (advance_lights(P, L, true, vis)) {
-                need_trace = true;
-                continue;
-            }
+            run_lights = true;
+            lights_have = true;
+            lights_vis = vis;
         } else {
             // a getFinalColor node (src/main.cpp:131-190)
             L.cur_d = L.qd;
             if (!hit) {
                 L.color = v3{0.0f, 0.0f, 0.0f};
+                node_hit = false;
             } else {
                 if (COUNT) cnt.hits++;
                 const Surf s = surface(S, L.qo, L.qd, b);
@@ -639,74 +800,43 @@ __global__ __launch_bounds__(64, WPE) void persistent_kernel(KParams P, JobSrc J
                 L.lt = L_POINT;
                 L.li = 0;
                 L.ls = -1;
-                if (advance_lights(P, L, false, false)) {
-                    need_trace = true;
-                    continue;
-                }
+                run_lights = true;
             }
-            // fall through to finish with hit/miss
-            v3 out;
-            if (finish_node(P, L, fr, hit, out)) {
-                need_trace = true;
-                continue;
-            }
-            // level-0 colour complete
-            if (J.mode == 0) {
-                if (P.aa || P.multi) L.pacc += out;
-                else L.pacc = out;
-                L.sample++;
-                if (L.sample < L.nsamples) {
-                    queue_camera(P, L);
-                    need_trace = true;
-                    continue;
-                }
-                v3 col = L.pacc;
-                if (P.aa) col = L.pacc * 0.25f;
-                else if (P.multi) col = L.pacc * (float)(1.0f / (float)P.sample_size);
-                float* dst = P.out + ((size_t)L.out_row * P.W + L.px) * 3;
-                dst[0] = col.x;
-                dst[1] = col.y;
-                dst[2] = col.z;
-            } else {
-                J.rgb[L.job * 3 + 0] = out.x;
-                J.rgb[L.job * 3 + 1] = out.y;
-                J.rgb[L.job * 3 + 2] = out.z;
-                J.ray_counts[L.job] = job_cnt.rays;
-            }
-            L.job = -1;
+        }
+        if (run_lights && advance_lights(P, L, lights_have, lights_vis)) {
+            need_trace = true;
             continue;
         }
-        // shadow path finished every light: the node is complete
-        {
-            v3 out;
-            if (finish_node(P, L, fr, true, out)) {
+        // every light done (or a miss): fold the node into the recursion tree
+        v3 out;
+        if (finish_node(P, L, fr, node_hit, out)) {
+            need_trace = true;
+            continue;
+        }
+        // level-0 colour complete
+        if (J.mode == 0) {
+            if (P.aa || P.multi) L.pacc += out;
+            else L.pacc = out;
+            L.sample++;
+            if (L.sample < L.nsamples) {
+                queue_camera(P, L);
                 need_trace = true;
                 continue;
             }
-            if (J.mode == 0) {
-                if (P.aa || P.multi) L.pacc += out;
-                else L.pacc = out;
-                L.sample++;
-                if (L.sample < L.nsamples) {
-                    queue_camera(P, L);
-                    need_trace = true;
-                    continue;
-                }
-                v3 col = L.pacc;
-                if (P.aa) col = L.pacc * 0.25f;
-                else if (P.multi) col = L.pacc * (float)(1.0f / (float)P.sample_size);
-                float* dst = P.out + ((size_t)L.out_row * P.W + L.px) * 3;
-                dst[0] = col.x;
-                dst[1] = col.y;
-                dst[2] = col.z;
-            } else {
-                J.rgb[L.job * 3 + 0] = out.x;
-                J.rgb[L.job * 3 + 1] = out.y;
-                J.rgb[L.job * 3 + 2] = out.z;
-                J.ray_counts[L.job] = job_cnt.rays;
-            }
-            L.job = -1;
+            v3 col = L.pacc;
+            if (P.aa) col = L.pacc * 0.25f;
+            else if (P.multi) col = L.pacc * (float)(1.0f / (float)P.sample_size);
+            float* dst = P.out + ((size_t)L.out_row * P.W + L.px) * 3;
+            dst[0] = col.x;
+            dst[1] = col.y;
+            dst[2] = col.z;
+        } else {
+            J.rgb[L.job * 3 + 0] = out.x;
+            J.rgb[L.job * 3 + 1] = out.y;
+            J.rgb[L.job * 3 + 2] = out.z;
+            J.ray_counts[L.job] = job_cnt.rays;
         }
+        L.job = -1;
     }
     flush_counters<COUNT>(P, cnt);
 }

@@ -23,6 +23,8 @@ struct rt_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     DevScene S{};
+    DevScene S8{};  // same scene, nodes/records of the quantised wide BVH (bw > 2)
+    int bw = 8;     // BVH width the persistent kernel walks (fixed at rt_create)
     std::vector<void*> allocs;
     unsigned long long* d_stats = nullptr;
     float* d_fb = nullptr;
@@ -41,30 +43,56 @@ struct rt_ctx {
 static int wpe() {
     const char* w = std::getenv("RT_WPE");
     const int v = w ? std::atoi(w) : 2;
-    return (v >= 1 && v <= 4) ? v : 2;
+    return (v == 1) ? 1 : 2;
+}
+
+// BVH the persistent kernel walks, read once at rt_create: 8 (quantised 8-wide, default),
+// 4 (same node format, 4 slots) or 2 (binary, full-precision boxes); RT_BVH selects for A/B runs
+static int bvh_width_env() {
+    const char* b = std::getenv("RT_BVH");
+    const int v = b ? std::atoi(b) : 8;
+    return (v == 2 || v == 4) ? v : 8;
+}
+
+template <bool COUNT, int BW>
+static void launch_wide(int grid, hipStream_t st, const KParams& K, const JobSrc& J) {
+    if (wpe() == 1)
+        hipLaunchKernelGGL((persistent_kernel<COUNT, 1, BW>), dim3(grid), dim3(64), 0, st, K, J);
+    else
+        hipLaunchKernelGGL((persistent_kernel<COUNT, 2, BW>), dim3(grid), dim3(64), 0, st, K, J);
 }
 
 template <bool COUNT>
-static void launch_persistent(int grid, hipStream_t st, const KParams& K, const JobSrc& J) {
-    switch (wpe()) {
-        case 1: hipLaunchKernelGGL((persistent_kernel<COUNT, 1>), dim3(grid), dim3(64), 0, st, K, J); break;
-        case 3: hipLaunchKernelGGL((persistent_kernel<COUNT, 3>), dim3(grid), dim3(64), 0, st, K, J); break;
-        case 4: hipLaunchKernelGGL((persistent_kernel<COUNT, 4>), dim3(grid), dim3(64), 0, st, K, J); break;
-        default: hipLaunchKernelGGL((persistent_kernel<COUNT, 2>), dim3(grid), dim3(64), 0, st, K, J); break;
+static void launch_persistent(int grid, hipStream_t st, KParams K, const JobSrc& J, const rt_ctx* c) {
+    if (c->bw > 2) {
+        K.S = c->S8;
+        if (c->bw == 4)
+            launch_wide<COUNT, 4>(grid, st, K, J);
+        else
+            launch_wide<COUNT, 8>(grid, st, K, J);
+    } else {
+        if (wpe() == 1)
+            hipLaunchKernelGGL((persistent_kernel<COUNT, 1, 2>), dim3(grid), dim3(64), 0, st, K, J);
+        else
+            hipLaunchKernelGGL((persistent_kernel<COUNT, 2, 2>), dim3(grid), dim3(64), 0, st, K, J);
     }
 }
 
 static int persistent_grid(rt_ctx* c) {
+    if (const char* g = std::getenv("RT_GRID")) {  // A/B override: blocks per CU
+        int cus = 0;
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
+        return std::max(1, cus) * std::max(1, std::atoi(g));
+    }
     if (c->persistent_blocks[wpe()] > 0) return c->persistent_blocks[wpe()];
     int cus = 0, per_cu = 0;
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
     hipError_t e = hipErrorInvalidValue;
-    switch (wpe()) {
-        case 1: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_kernel<false, 1>, 64, 0); break;
-        case 3: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_kernel<false, 3>, 64, 0); break;
-        case 4: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_kernel<false, 4>, 64, 0); break;
-        default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_kernel<false, 2>, 64, 0); break;
-    }
+    // every BVH width compiles to the same LDS footprint and register cap per WPE
+    if (wpe() == 1)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_kernel<false, 1, 8>, 64, 0);
+    else
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_kernel<false, 2, 8>, 64, 0);
     if (e != hipSuccess || per_cu <= 0) per_cu = 8;
     c->persistent_blocks[wpe()] = std::max(1, cus) * per_cu;
     return c->persistent_blocks[wpe()];
@@ -200,22 +228,41 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
     c->nrec = ntri;
 
     // --- triangle records (64 B): v0|n.x, v1|n.y, v2|n.z, D|key_brute|key_bvh|ref_leaf ---
-    std::vector<float> rec((size_t)ntri * 16);
-    for (int r = 0; r < ntri; ++r) {
-        const int t = bvh.order[r];
-        const float* p = desc->positions + (size_t)t * 9;
-        const v3 v0{p[0], p[1], p[2]}, v1{p[3], p[4], p[5]}, v2{p[6], p[7], p[8]};
-        // trianglePlane (src/ray_tracing.cpp:91-100)
-        const v3 n = normalize(cross(v0 - v2, v1 - v2));
-        const float D = dot(n, v0);
-        float* o = rec.data() + (size_t)r * 16;
-        o[0] = v0.x; o[1] = v0.y; o[2] = v0.z; o[3] = n.x;
-        o[4] = v1.x; o[5] = v1.y; o[6] = v1.z; o[7] = n.y;
-        o[8] = v2.x; o[9] = v2.y; o[10] = v2.z; o[11] = n.z;
-        int ib[4] = {0, t, ref.tri_key[t], ref.tri_leaf[t]};
-        std::memcpy(&o[12], &D, 4);
-        std::memcpy(&o[13], &ib[1], 12);
+    auto make_records = [&](const std::vector<int>& order) {
+        std::vector<float> rec((size_t)ntri * 16);
+        for (int r = 0; r < ntri; ++r) {
+            const int t = order[r];
+            const float* p = desc->positions + (size_t)t * 9;
+            const v3 v0{p[0], p[1], p[2]}, v1{p[3], p[4], p[5]}, v2{p[6], p[7], p[8]};
+            // trianglePlane (src/ray_tracing.cpp:91-100)
+            const v3 n = normalize(cross(v0 - v2, v1 - v2));
+            const float D = dot(n, v0);
+            float* o = rec.data() + (size_t)r * 16;
+            o[0] = v0.x; o[1] = v0.y; o[2] = v0.z; o[3] = n.x;
+            o[4] = v1.x; o[5] = v1.y; o[6] = v1.z; o[7] = n.y;
+            o[8] = v2.x; o[9] = v2.y; o[10] = v2.z; o[11] = n.z;
+            int ib[4] = {0, t, ref.tri_key[t], ref.tri_leaf[t]};
+            std::memcpy(&o[12], &D, 4);
+            std::memcpy(&o[13], &ib[1], 12);
+        }
+        return rec;
+    };
+    const std::vector<float> rec = make_records(bvh.order);
+    c->bw = bvh_width_env();
+    Bvh8 bvh8;
+    try {
+        if (c->bw > 2) bvh8 = build_bvh8(bvh, c->bw);
+    } catch (const std::exception& ex) {
+        set_error(std::string("rt_create: ") + ex.what());
+        delete c;
+        return RT_ERR_INVALID;
     }
+    if (c->bw > 2 && (bvh8.max_depth + 2 >= RT_STACK_SIZE || (int)bvh8.order.size() != ntri)) {
+        set_error("rt_create: BVH8 deeper than the traversal stack");
+        delete c;
+        return RT_ERR_INVALID;
+    }
+    const std::vector<float> rec8 = c->bw > 2 ? make_records(bvh8.order) : std::vector<float>();
     std::vector<float> nodes((size_t)bvh.nodes.size() * 16);
     for (size_t i = 0; i < bvh.nodes.size(); ++i) {
         const Bvh2Node& nd = bvh.nodes[i];
@@ -306,7 +353,16 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
     S.nplane = desc->num_plane_lights;
     S.all_opaque = all_opaque ? 1 : 0;
 
-    if (hipMalloc(&c->d_stats, 8 * sizeof(unsigned long long)) != hipSuccess ||
+    // 8-wide variant: same scene, records permuted into the BVH8 leaf order
+    c->S8 = S;
+    const float4* d_rec8 = nullptr;
+    const float4* d_nodes8 = nullptr;
+    UP(reinterpret_cast<const float4*>(rec8.data()), rec8.size() / 4, d_rec8);
+    UP(reinterpret_cast<const float4*>(bvh8.nodes.data()), bvh8.nodes.size() / 4, d_nodes8);
+    c->S8.tri = d_rec8;
+    c->S8.nodes = d_nodes8;
+
+    if (hipMalloc(&c->d_stats, 16 * sizeof(unsigned long long)) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
         set_error("rt_create: HIP allocation failed");
@@ -390,7 +446,7 @@ static int launch_render(rt_ctx* c, KParams& K, hipStream_t st, int count_mode, 
     const int tiles_x = (K.W + 7) / 8;
     const int tiles_y = (K.band_rows + 7) / 8;
     const long long blocks = (long long)tiles_x * tiles_y * K.n_local_bands;
-    HIP_TRY(hipMemsetAsync(c->d_stats, 0, 8 * sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(c->d_stats, 0, 16 * sizeof(unsigned long long), st));
     if (blocks > 0) {
         HIP_TRY(hipEventRecord(c->ev0, st));
         if (use_tile_kernel()) {
@@ -402,12 +458,12 @@ static int launch_render(rt_ctx* c, KParams& K, hipStream_t st, int count_mode, 
             JobSrc J{};
             J.mode = 0;
             J.njobs = (int)(blocks * 64);
-            J.counter = reinterpret_cast<int*>(c->d_stats + 6);
+            J.counter = reinterpret_cast<int*>(c->d_stats + 7);
             const int grid = (int)std::min<long long>(blocks, persistent_grid(c));
             if (count_mode)
-                launch_persistent<true>(grid, st, K, J);
+                launch_persistent<true>(grid, st, K, J, c);
             else
-                launch_persistent<false>(grid, st, K, J);
+                launch_persistent<false>(grid, st, K, J, c);
         }
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(c->ev1, st));
@@ -553,10 +609,10 @@ extern "C" int rt_shade(rt_ctx* c, const rt_ray* rays, int n, const rt_params* p
         J.rays = d_r;
         J.rgb = d_c;
         J.ray_counts = d_n;
-        J.counter = reinterpret_cast<int*>(c->d_stats + 6);
-        hipMemsetAsync(c->d_stats, 0, 8 * sizeof(unsigned long long), c->stream);
+        J.counter = reinterpret_cast<int*>(c->d_stats + 7);
+        hipMemsetAsync(c->d_stats, 0, 16 * sizeof(unsigned long long), c->stream);
         const int grid = std::min((n + 63) / 64, persistent_grid(c));
-        launch_persistent<false>(grid, c->stream, K, J);
+        launch_persistent<false>(grid, c->stream, K, J, c);
     }
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
@@ -569,6 +625,16 @@ extern "C" int rt_shade(rt_ctx* c, const rt_ray* rays, int n, const rt_params* p
         set_error(std::string("rt_shade: ") + hipGetErrorString(e));
         return RT_ERR_HIP;
     }
+    return RT_OK;
+}
+
+// Debug counters of the last counting launch: [8..13] per-query node-visit histogram
+// (<16, <64, <256, <1024, <4096, >=4096), [14] max node visits, [15] max triangle records.
+extern "C" int rt_debug_counters(rt_ctx* c, uint64_t* out, int n) {
+    if (!c || !out || n <= 0) return RT_ERR_INVALID;
+    unsigned long long h[16] = {0};
+    HIP_TRY(hipMemcpy(h, c->d_stats, sizeof(h), hipMemcpyDeviceToHost));
+    for (int i = 0; i < n && i < 16; ++i) out[i] = h[i];
     return RT_OK;
 }
 

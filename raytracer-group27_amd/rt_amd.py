@@ -100,7 +100,7 @@ EXPORTS = [
     "rt_scene_add_spot_light", "rt_scene_add_plane_light", "rt_scene_clear_lights", "rt_scene_set_material",
     "rt_scene_desc_get", "rt_scene_free", "rt_write_dragon_proxy", "rt_camera_from_trackball", "rt_create",
     "rt_destroy", "rt_render", "rt_render_device", "rt_unpermute_bands_device", "rt_intersect", "rt_shade",
-    "rt_set_counting", "rt_ctx_info", "rt_selftest_math",
+    "rt_set_counting", "rt_debug_counters", "rt_ctx_info", "rt_selftest_math",
 ]
 
 _lib = None
@@ -142,6 +142,7 @@ def lib():
             "rt_intersect": ([vp, vp, C.c_int, C.c_int, vp], C.c_int),
             "rt_shade": ([vp, vp, C.c_int, P(rt_params), P(C.c_float), P(C.c_uint64)], C.c_int),
             "rt_set_counting": ([C.c_int], C.c_int),
+            "rt_debug_counters": ([vp, P(C.c_uint64), C.c_int], C.c_int),
             "rt_ctx_info": ([vp, P(C.c_int), P(C.c_int), P(C.c_int), P(C.c_int)], C.c_int),
             "rt_selftest_math": ([vp, P(C.c_float), P(C.c_float), C.c_int, P(C.c_float)], C.c_int),
         }
@@ -327,6 +328,11 @@ class Context:
                              rgb.ctypes.data_as(C.POINTER(C.c_float)),
                              cnt.ctypes.data_as(C.POINTER(C.c_uint64))), "rt_shade")
         return rgb.reshape(-1, 3), cnt
+
+    def debug_counters(self):
+        out = np.zeros(16, np.uint64)
+        check(lib().rt_debug_counters(self.h, out.ctypes.data_as(C.POINTER(C.c_uint64)), 16))
+        return out
 
     def selftest_math(self, x, y):
         x = np.ascontiguousarray(x, np.float32)
