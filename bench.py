@@ -27,9 +27,26 @@ BAND_ROWS = 8
 
 
 def algorithmic_bytes(st, pixels):
-    """64 B per BVH2 node visit, 64 B per triangle record, 68 B per shaded hit
-    (3 normals + material), 12 B per pixel written."""
-    return 64 * st.node_visits + 64 * st.tri_tests + 68 * st.hits + 12 * pixels
+    """one node record per node visit (64 B BVH2, 128 B quantised BVH8 -- the
+    structure the kernel walks), 64 B per triangle record, 68 B per shaded hit (3 normals +
+    material), 12 B per pixel written."""
+    return int(st.node_bytes or 64) * st.node_visits + 64 * st.tri_tests + 68 * st.hits + 12 * pixels
+
+
+def kernel_name(ntri):
+    """Name of the dominant kernel as rocprofv3 lists it (rt_runtime.hip: RT_KERNEL / RT_WPE / RT_BVH;
+    by default whole-traversal refill below 65 536 triangles, dynamic fetch above)."""
+    k = os.environ.get("RT_KERNEL")
+    if k == "tile":
+        return "rt::render_kernel<false>"
+    wpe = 1 if os.environ.get("RT_WPE") == "1" else 2
+    bw = os.environ.get("RT_BVH", "8")
+    bw = bw if bw in ("2", "4") else "8"
+    if k == "wavefront":
+        return f"rt::wf_trace_kernel<false, 4, {bw}>"
+    if k == "persistent" or (k != "df" and ntri < 65536) or bw == "2":
+        return f"rt::persistent_kernel<false, {wpe}, {bw}>"
+    return f"rt::persistent_df_kernel<false, {wpe}, {bw}>"
 
 
 def cpu_baseline(config, budget_s=12.0, seed=12345):
@@ -71,13 +88,14 @@ def _cpu_model():
     return "unknown"
 
 
-def load_pmc(config):
-    """HBM bytes per render launch from a committed rocprofv3 --pmc run (tools/profile.sh), or None."""
+def load_pmc(config, kernel):
+    """HBM bytes per render launch from the committed rocprofv3 --pmc summary of the same kernel
+    (tools/profile.sh + tools/pmc_summary.py --latest), or None."""
     p = os.path.join(REPO, "profiles", "pmc_latest.json")
     try:
         with open(p) as f:
             d = json.load(f)
-        if d.get("config") == config:
+        if d.get("config") == config and kernel in (d.get("kernel") or ""):
             return d.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
@@ -168,7 +186,8 @@ def main():
         bytes0 = algorithmic_bytes(cst, min(pixels0, W * H))
         avg_ms = float(np.mean(kms))
         achieved = bytes0 / (avg_ms * 1e-3) / 1e9
-        pmc = load_pmc(args.config)
+        kname = kernel_name(ctx.info()["tri_records"])
+        pmc = load_pmc(args.config, kname)
         line = {
             "metric": METRIC,
             "value": total_rays / max_elapsed / 1e6,
@@ -188,7 +207,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": (float(pmc) if pmc is not None else None),
-                         "kernel": "render_kernel<false>", "kernel_avg_ms": avg_ms,
+                         "kernel": kname, "kernel_avg_ms": avg_ms,
                          "algorithmic_bytes_per_launch": int(bytes0)},
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -142,11 +142,13 @@ typedef struct rt_hit {
 /* Per-launch counters (rt_render_device / rt_render). */
 typedef struct rt_stats {
     uint64_t rays;          /* intersect() calls: primary + secondary + shadow segments */
-    uint64_t node_visits;   /* BVH2 nodes fetched (counting builds only, else 0) */
+    uint64_t node_visits;   /* BVH nodes fetched (counting builds only, else 0) */
     uint64_t tri_tests;     /* triangle records fetched (counting builds only, else 0) */
     uint64_t hits;          /* closest hits shaded (counting builds only, else 0) */
     float kernel_ms;        /* device time of the render launch(es), HIP events */
-    float pad_;
+    uint32_t node_bytes;    /* bytes per node record of the BVH walked: 64 (BVH2), 128 (quantised BVH8) */
+    float trace_ms;         /* wavefront path: device time of the trace launches (HIP events), else 0 */
+    uint32_t trace_launches;/* wavefront path: trace launches of the frame */
 } rt_stats;
 
 typedef struct rt_ctx rt_ctx;

@@ -89,11 +89,22 @@ struct KParams {
     int band_rows, band_rank, band_count, n_local_bands;
     float* out;
     unsigned long long* stats;  // rays, node visits, tri tests, hits
+    int refill;                 // dynamic-fetch kernel: waiting lanes that end a traversal phase
+    int leaf_batch;             // dynamic-fetch kernel: lanes with postponed leaves that start a leaf phase
+    const float* pre_t;         // precomputed primary hits per job (rt_packet.hip), or null
+    const int* pre_rec;
 };
 
 struct Cnt {
     uint32_t rays, nodes, tris, hits;
+    uint32_t wnodes, wtris, wadv;  // wave-level steps (counted by the first active lane): SIMD efficiency
+    unsigned long long cyc_a, cyc_b;  // shader clocks per wave in the state machine / in traversal (df kernel)
 };
+
+// true on the lowest active lane of the wave (counting builds: one count per wave instruction stream)
+__device__ __forceinline__ bool wave_leader() {
+    return (int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1;
+}
 
 // ------------------------------------------------------------------------------------------
 // Reference slab test (src/ray_tracing.cpp:213-264), dir = normalize(ray.direction).
@@ -150,6 +161,7 @@ struct Best {
 };
 
 #define RT_NO_HIT (-0x7fffffff - 1)
+#define RT_PRE_NONE (-0x7fffffff)  // INT_MIN + 1: no precomputed primary hit (rt_packet.hip); trace it
 
 // Reference triangle test for one record.  Returns true and the reference t when the
 // reference would accept the triangle with ray.t = +inf (order-free part).
@@ -674,12 +686,25 @@ __device__ void flush_counters(const KParams& P, const Cnt& c) {
             h += __shfl_xor(h, off);
         }
     }
+    unsigned long long wn = c.wnodes, wt = c.wtris, wa = c.wadv;
+    if (COUNT) {
+        for (int off = 32; off > 0; off >>= 1) {
+            wn += __shfl_xor(wn, off);
+            wt += __shfl_xor(wt, off);
+            wa += __shfl_xor(wa, off);
+        }
+    }
     if ((threadIdx.x & 63) == 0) {
         atomicAdd(P.stats + 0, r);
         if (COUNT) {
             atomicAdd(P.stats + 1, nv);
             atomicAdd(P.stats + 2, tt);
             atomicAdd(P.stats + 3, h);
+            atomicAdd(P.stats + 4, wn);
+            atomicAdd(P.stats + 5, wt);
+            atomicAdd(P.stats + 6, wa);
+            atomicAdd(P.stats + 8, c.cyc_a);
+            atomicAdd(P.stats + 9, c.cyc_b);
         }
     }
 }

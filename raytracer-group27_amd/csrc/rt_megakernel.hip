@@ -85,7 +85,10 @@ __device__ __forceinline__ bool trace_query(const DevScene& S, v3 o, v3 d, float
             const float4 e = np[3];
             const int c0 = __float_as_int(e.x), c1 = __float_as_int(e.y);
             const int n0 = __float_as_int(e.z), n1 = __float_as_int(e.w);
-            if (COUNT) cnt.nodes++;
+            if (COUNT) {
+                cnt.nodes++;
+                if (wave_leader()) cnt.wnodes++;
+            }
             float tn0 = 0.0f, tn1 = 0.0f;
             bool h0 = (c0 >= 0) && box_hit(a.x, a.y, a.z, a.w, b.x, b.y, o, inv, tcull, tn0);
             bool h1 = (c1 >= 0) && box_hit(b.z, b.w, c.x, c.y, c.z, c.w, o, inv, tcull, tn1);
@@ -98,7 +101,10 @@ __device__ __forceinline__ bool trace_query(const DevScene& S, v3 o, v3 d, float
                 for (int r = c0; r < c0 + n0; ++r) {
                     const float4* tp = S.tri + r * 4;
                     const float4 r0 = tp[0], r1 = tp[1], r2 = tp[2], r3 = tp[3];
-                    if (COUNT) cnt.tris++;
+                    if (COUNT) {
+            cnt.tris++;
+            if (wave_leader()) cnt.wtris++;
+        }
                     float t;
                     if (!tri_test(r0, r1, r2, r3, o, d, nd, t)) continue;
                     const int key = REF ? __float_as_int(r3.z) : __float_as_int(r3.y);
@@ -141,7 +147,10 @@ __device__ __forceinline__ bool trace_query(const DevScene& S, v3 o, v3 d, float
         for (int r = first; r < first + count; ++r) {
             const float4* tp = S.tri + r * 4;
             const float4 r0 = tp[0], r1 = tp[1], r2 = tp[2], r3 = tp[3];
-            if (COUNT) cnt.tris++;
+            if (COUNT) {
+            cnt.tris++;
+            if (wave_leader()) cnt.wtris++;
+        }
             float t;
             if (!tri_test(r0, r1, r2, r3, o, d, nd, t)) continue;
             const int key = REF ? __float_as_int(r3.z) : __float_as_int(r3.y);
@@ -185,7 +194,10 @@ __device__ __forceinline__ bool test_records(const DevScene& S, int first, int c
     for (int r = first; r < first + count; ++r) {
         const float4* tp = S.tri + r * 4;
         const float4 r0 = tp[0], r1 = tp[1], r2 = tp[2], r3 = tp[3];
-        if (COUNT) cnt.tris++;
+        if (COUNT) {
+            cnt.tris++;
+            if (wave_leader()) cnt.wtris++;
+        }
         float t;
         if (!tri_test(r0, r1, r2, r3, o, d, nd, t)) continue;
         const int key = REF ? __float_as_int(r3.z) : __float_as_int(r3.y);
@@ -229,7 +241,10 @@ __device__ __forceinline__ bool trace_query8(const DevScene& S, v3 o, v3 d, floa
         for (;;) {
             const uint32_t node = cur >> 8;
             const float4 f0 = g0, f1 = g1, qlx = g2, qly = g3, qlz = g4, qhx = g5, qhy = g6, qhz = g7;
-            if (COUNT) cnt.nodes++;
+            if (COUNT) {
+                cnt.nodes++;
+                if (wave_leader()) cnt.wnodes++;
+            }
             const uint32_t w3 = __float_as_uint(f0.w);
             const uint32_t imask = __float_as_uint(f1.z) & 0xFFu;
             const uint32_t lmask = (__float_as_uint(f1.z) >> 8) & 0xFFu;
@@ -680,6 +695,8 @@ __global__ __launch_bounds__(64, WPE) void persistent_kernel(KParams P, JobSrc J
     Cnt cnt{0u, 0u, 0u, 0u};
     Cnt job_cnt{0u, 0u, 0u, 0u};  // per-job ray count (rt_shade)
     bool need_trace = false;
+    bool pre = false;  // the queued camera query's hit is precomputed (primary packet pass)
+    Best pb;
     for (;;) {
         // ---- refill idle lanes (one atomic per wave) ----
         const bool idle = (L.job < 0);
@@ -704,6 +721,15 @@ __global__ __launch_bounds__(64, WPE) void persistent_kernel(KParams P, JobSrc J
                             L.nsamples = P.aa ? 4 : (P.multi ? P.sample_size : 1);
                             queue_camera(P, L);
                             need_trace = true;
+                            if (P.pre_rec) {
+                                const int r = P.pre_rec[job];
+                                if (r != RT_PRE_NONE) {
+                                    pre = true;
+                                    pb.t = P.pre_t[job];
+                                    pb.rec = r;
+                                    pb.key = 0;
+                                }
+                            }
                         }
                     } else {
                         const rt_ray r = J.rays[job];
@@ -729,7 +755,11 @@ __global__ __launch_bounds__(64, WPE) void persistent_kernel(KParams P, JobSrc J
         // ---- the one traversal ----
         Best b;
         bool hit = false;
-        if (busy) {
+        if (busy && pre) {
+            b = pb;
+            hit = (pb.rec != RT_NO_HIT);
+            pre = false;
+        } else if (busy) {
             cnt.rays++;
             job_cnt.rays++;
             const bool shadow = (L.qtype == Q_SHADOW);
@@ -742,6 +772,7 @@ __global__ __launch_bounds__(64, WPE) void persistent_kernel(KParams P, JobSrc J
                 hit = trace_query<COUNT>(S, L.qo, L.qd, L.qt, thr, ref, any, b, stk, cnt);
         }
         if (!busy) continue;
+        if (COUNT && wave_leader()) cnt.wadv++;
         // ---- advance the state machine until the next query ----
         // Each step below has exactly one call site (advance_lights, finish_node, pixel output):
         // inlined twice, the light loop and the recursion fold pushed the kernel past 256 VGPRs.
@@ -837,6 +868,434 @@ __global__ __launch_bounds__(64, WPE) void persistent_kernel(KParams P, JobSrc J
             J.ray_counts[L.job] = job_cnt.rays;
         }
         L.job = -1;
+    }
+    flush_counters<COUNT>(P, cnt);
+}
+
+
+// ---- dynamic-fetch persistent kernel (quantised BVH8/BVH4) ------------------------------------
+// persistent_kernel above refills a lane only between whole traversals, so a wave runs every
+// traversal for as long as its slowest query: on the dragon ~1/5 of the lanes are active per
+// node fetch.  Here the traversal is a resumable per-lane state (Trav) advanced one node visit
+// per iteration; a lane whose query completes parks as "pending", and once `refill` lanes of the
+// wave are pending (or none is still tracing) the wave leaves the traversal loop, advances every
+// pending lane's state machine to its next query (or next pixel), and resumes.  Every query is
+// still judged with the same arithmetic and (t, key) order as trace_query8, so the image and the
+// ray count are bit-identical; only the interleaving of queries within a wave changes.
+#define RT_TRAV_NONE 0xFFFFFFFFu
+
+struct Trav {
+    v3 o, d, nd, inv;
+    float thr, tcull;
+    Best best;
+    RefMask mask;
+    uint32_t cur;  // node << 8 | slot mask of the node to visit next; RT_TRAV_NONE: none
+    int sp;        // LDS stack depth (groups node << 8 | inner slots not yet visited)
+    // postponed leaf work: the record cursor of the current range, then the hit leaf slots
+    // (lh) of the last visited node whose records start at lb with 4-bit counts lc
+    int rr, rk;
+    uint32_t lb, lc, lh;
+    bool found, ref, any;
+};
+
+__device__ __forceinline__ bool leaf_pending(const Trav& T) { return T.rk > 0 || T.lh != 0u; }
+
+// Query setup: the prologue of trace_query8 / trace_query (same thresholds and flags).
+__device__ __forceinline__ void trav_init_q(const DevScene& S, bool use_bvh, v3 qo, v3 qd, float qt, bool shadow,
+                                            float sdist, Trav& T) {
+    T.o = qo;
+    T.d = qd;
+    T.nd = normalize(qd);
+    T.inv = safe_inv(qd);
+    T.ref = shadow || use_bvh;
+    T.any = shadow && S.all_opaque;
+    T.thr = sdist - 2.0f * 0.0005f;
+    T.best.t = qt;
+    T.best.key = -1;
+    T.best.rec = RT_NO_HIT;
+    T.mask = RefMask{0u, 0u};
+    T.tcull = T.any ? T.thr : qt;
+    T.found = false;
+    T.sp = 0;
+    T.lb = 0u;
+    T.lc = 0u;
+    T.lh = 0u;
+    const float dd = dot(qd, qd);
+    if (!(fabsf(dd - 1.0f) <= 4e-6f)) {  // non-unit direction: exhaustive (see traverse())
+        T.rr = 0;
+        T.rk = S.ntri;
+        T.cur = RT_TRAV_NONE;
+    } else {
+        T.rr = 0;
+        T.rk = 0;
+        T.cur = (S.ntri > 0) ? 0xFFu : RT_TRAV_NONE;
+    }
+}
+
+__device__ __forceinline__ void trav_init(const KParams& P, const Lane& L, Trav& T) {
+    trav_init_q(P.S, P.use_bvh != 0, L.qo, L.qd, L.qt, L.qtype == Q_SHADOW, L.sdist, T);
+}
+
+__device__ __forceinline__ void node_fetch(const float4* nodes, uint32_t cur, float4 (&g)[8]) {
+    const float4* np = nodes + (size_t)(cur >> 8) * 8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) g[k] = np[k];
+}
+
+// One node visit (node in g): box tests of its slots, the next node (whose 128 B are requested
+// at once into g), and the hit leaf slots postponed into T.lb/lc/lh.
+// PF: the node was prefetched into g by the previous visit (and the next one is prefetched here);
+// otherwise it is loaded now (fewer live registers).
+template <bool COUNT, int NW, bool PF = true>
+__device__ __forceinline__ void trav_node(const DevScene& S, Trav& T, int* stk, float4 (&g)[8], Cnt& cnt) {
+    const uint32_t node = T.cur >> 8;
+    if (!PF) node_fetch(S.nodes, T.cur, g);
+    const float4 f0 = g[0], f1 = g[1], qlx = g[2], qly = g[3], qlz = g[4], qhx = g[5], qhy = g[6], qhz = g[7];
+    if (COUNT) {
+        cnt.nodes++;
+        if (wave_leader()) cnt.wnodes++;
+    }
+    const v3 o = T.o, inv = T.inv;
+    const uint32_t w3 = __float_as_uint(f0.w);
+    const uint32_t imask = __float_as_uint(f1.z) & 0xFFu;
+    const uint32_t lmask = (__float_as_uint(f1.z) >> 8) & 0xFFu;
+    const uint32_t child_base = __float_as_uint(f1.x);
+    const float bx = pow2f(w3 & 0xFFu) * inv.x, by = pow2f((w3 >> 8) & 0xFFu) * inv.y,
+                bz = pow2f((w3 >> 16) & 0xFFu) * inv.z;
+    const float ax = (f0.x - o.x) * inv.x, ay = (f0.y - o.y) * inv.y, az = (f0.z - o.z) * inv.z;
+    const uint32_t m = (T.cur & 0xFFu) & (imask | lmask);
+    const float tcull = T.tcull;
+    uint32_t hits = 0;
+    float tbest = FLT_MAX;
+    int sbest = -1;
+#pragma unroll
+    for (int s = 0; s < NW; ++s) {
+        if (m & (1u << s)) {
+            const int wi = s >> 1, sh = (s & 1) * 16;
+            auto q = [&](const float4& f) {
+                const uint32_t wv = __float_as_uint(wi == 0 ? f.x : wi == 1 ? f.y : wi == 2 ? f.z : f.w);
+                return (float)((wv >> sh) & 0xFFFFu);
+            };
+            const float tlx = fmaf(q(qlx), bx, ax), thx = fmaf(q(qhx), bx, ax);
+            const float tly = fmaf(q(qly), by, ay), thy = fmaf(q(qhy), by, ay);
+            const float tlz = fmaf(q(qlz), bz, az), thz = fmaf(q(qhz), bz, az);
+            const float t0 = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fminf(tlz, thz));
+            const float t1 = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fmaxf(tlz, thz));
+            if (t0 <= t1 && t1 >= 0.0f && t0 <= tcull) {
+                hits |= 1u << s;
+                if ((imask & (1u << s)) && (t0 < tbest || sbest < 0)) {
+                    tbest = t0;
+                    sbest = s;
+                }
+            }
+        }
+    }
+    T.lb = __float_as_uint(f1.y);
+    T.lc = __float_as_uint(f1.w);
+    T.lh = hits & lmask;
+    const uint32_t ih = hits & imask;
+    if (ih) {
+        const uint32_t rest = ih & ~(1u << sbest);
+        if (rest) {
+            stk[T.sp * RT_WAVE] = (int)((node << 8) | rest);
+            ++T.sp;
+        }
+        const uint32_t rank = __popc(imask & ((1u << sbest) - 1u));
+        T.cur = ((child_base + rank) << 8) | 0xFFu;
+    } else if (T.sp > 0) {
+        --T.sp;
+        T.cur = (uint32_t)stk[T.sp * RT_WAVE];
+    } else {
+        T.cur = RT_TRAV_NONE;
+    }
+    if (PF && T.cur != RT_TRAV_NONE) node_fetch(S.nodes, T.cur, g);
+}
+
+// One postponed leaf record (the loop body of test_records).  The cursor moves to the next hit
+// leaf slot when the current range is used up.  Any-hit queries drop the rest of their work on
+// the first accepted candidate.
+template <bool COUNT>
+__device__ __forceinline__ void trav_record(const DevScene& S, Trav& T, Cnt& cnt) {
+    if (T.rk == 0) {
+        const int s = __ffs(T.lh) - 1;
+        T.lh &= T.lh - 1u;
+        const uint32_t below = s ? (T.lc & ((1u << (4 * s)) - 1u)) : 0u;
+        uint32_t nib = (below & 0x0F0F0F0Fu) + ((below >> 4) & 0x0F0F0F0Fu);
+        nib = (nib * 0x01010101u) >> 24;
+        T.rr = (int)(T.lb + nib);
+        T.rk = (int)((T.lc >> (4 * s)) & 15u);
+        if (T.rk == 0) return;
+    }
+    const int r = T.rr;
+    T.rr = r + 1;
+    T.rk--;
+    const float4* tp = S.tri + r * 4;
+    const float4 r0 = tp[0], r1 = tp[1], r2 = tp[2], r3 = tp[3];
+    if (COUNT) {
+        cnt.tris++;
+        if (wave_leader()) cnt.wtris++;
+    }
+    float t;
+    if (!tri_test(r0, r1, r2, r3, T.o, T.d, T.nd, t)) return;
+    const int key = T.ref ? __float_as_int(r3.z) : __float_as_int(r3.y);
+    if (T.any ? !(t <= T.thr) : !(t < T.best.t || (t == T.best.t && key < T.best.key))) return;
+    if (T.ref && !leaf_reachable(S, __float_as_int(r3.w), T.o, T.nd, T.mask)) return;
+    T.best.t = t;
+    T.best.key = key;
+    T.best.rec = r;
+    T.found = true;
+    if (T.any) {
+        T.rk = 0;
+        T.lh = 0u;
+        T.cur = RT_TRAV_NONE;
+    } else {
+        T.tcull = t;
+    }
+}
+
+// Epilogue of trace_query8: the spheres, after every triangle (same order and keys).
+__device__ __forceinline__ void trav_finish(const DevScene& S, Trav& T) {
+    if (T.any && T.found) return;
+    for (int s = 0; s < S.nsph; ++s) {
+        const DSph sp_ = S.sph[s];
+        float t;
+        if (!sphere_test(sp_, T.o, T.d, t)) continue;
+        const int key = T.ref ? sp_.key_bvh : S.ntri + s;
+        if (T.any ? !(t <= T.thr) : !(t < T.best.t || (t == T.best.t && key < T.best.key))) continue;
+        if (T.ref && !leaf_reachable(S, sp_.leaf, T.o, T.nd, T.mask)) continue;
+        T.best.t = t;
+        T.best.key = key;
+        T.best.rec = -s - 1;
+        T.found = true;
+        if (T.any) break;
+    }
+}
+
+// The state-machine advance of persistent_kernel after a finished query (shadow segment,
+// light loop, recursion fold, pixel output).  Returns true with the next query in L.q*; false
+// when the lane's job is complete (L.job = -1).
+template <bool COUNT>
+__device__ bool advance_lane(const KParams& P, const JobSrc& J, Lane& L, Frame* fr, bool hit, const Best& b,
+                             Cnt& cnt, const Cnt& job_cnt) {
+    const DevScene& S = P.S;
+    bool run_lights = false, lights_have = false, lights_vis = false;
+    bool node_hit = true;
+    if (L.qtype == Q_SHADOW) {
+        bool vis;
+        if (S.all_opaque) {
+            vis = !hit;
+        } else if (!hit || b.t > L.sdist - 2.0f * 0.0005f) {
+            vis = true;
+        } else {
+            const Surf s = surface(S, L.qo, L.qd, b);
+            if (s.m.transp != 1.0f) {
+                L.sdist -= b.t;
+                L.so = s.p + 0.0005f * L.sd;
+                const float c = fabsf(dot(L.sd, s.n));
+                const float R0 = s.m.transp;
+                L.sI = (float)((double)L.sI *
+                               (1.0 - ((double)R0 + (double)(1.0f - R0) * pow((double)(1.0f - c), 5.0))));
+                if (L.sdist > 0.0005f) {
+                    L.qo = L.so;
+                    L.qd = L.sd;
+                    L.qt = FLT_MAX;
+                    return true;
+                }
+                vis = true;  // loop exit without an opaque blocker
+            } else {
+                vis = false;
+            }
+        }
+        run_lights = true;
+        lights_have = true;
+        lights_vis = vis;
+    } else {
+        // a getFinalColor node (src/main.cpp:131-190)
+        L.cur_d = L.qd;
+        if (!hit) {
+            L.color = v3{0.0f, 0.0f, 0.0f};
+            node_hit = false;
+        } else {
+            if (COUNT) cnt.hits++;
+            const Surf s = surface(S, L.qo, L.qd, b);
+            L.hp = s.p;
+            L.nN = normalize(s.n);
+            L.refl = reflect(normalize(L.qd), L.nN);
+            L.nR = normalize(L.refl);
+            L.mat = (b.rec >= 0) ? s.mesh : b.rec;
+            L.color = v3{0.0f, 0.0f, 0.0f};
+            L.lt = L_POINT;
+            L.li = 0;
+            L.ls = -1;
+            run_lights = true;
+        }
+    }
+    if (run_lights && advance_lights(P, L, lights_have, lights_vis)) return true;
+    v3 out;
+    if (finish_node(P, L, fr, node_hit, out)) return true;
+    // level-0 colour complete
+    if (J.mode == 0) {
+        if (P.aa || P.multi) L.pacc += out;
+        else L.pacc = out;
+        L.sample++;
+        if (L.sample < L.nsamples) {
+            queue_camera(P, L);
+            return true;
+        }
+        v3 col = L.pacc;
+        if (P.aa) col = L.pacc * 0.25f;
+        else if (P.multi) col = L.pacc * (float)(1.0f / (float)P.sample_size);
+        float* dst = P.out + ((size_t)L.out_row * P.W + L.px) * 3;
+        dst[0] = col.x;
+        dst[1] = col.y;
+        dst[2] = col.z;
+    } else {
+        J.rgb[L.job * 3 + 0] = out.x;
+        J.rgb[L.job * 3 + 1] = out.y;
+        J.rgb[L.job * 3 + 2] = out.z;
+        J.ray_counts[L.job] = job_cnt.rays;
+    }
+    L.job = -1;
+    return false;
+}
+
+template <bool COUNT, int WPE, int BW>
+__global__ __launch_bounds__(64, WPE) void persistent_df_kernel(KParams P, JobSrc J) {
+    __shared__ int stack_lds[RT_STACK_SIZE * RT_WAVE];
+    __shared__ int s_base;
+    const int lane_id = threadIdx.x;
+    int* stk = stack_lds + lane_id;
+    const DevScene& S = P.S;
+    Frame fr[RT_MAX_DEPTH];
+    Lane L;
+    L.job = -1;
+    Trav T;
+    Cnt cnt{0u, 0u, 0u, 0u};
+    Cnt job_cnt{0u, 0u, 0u, 0u};  // per-job ray count (rt_shade)
+    bool tracing = false;          // a query is in flight
+    bool pending = false;          // a finished query waits for advance_lane
+    const int refill_at = P.refill;
+    const int leaf_batch = P.leaf_batch;
+    for (;;) {
+        // ---- phase A: advance the pending lanes, then refill the idle ones ----
+        unsigned long long tA = COUNT ? (unsigned long long)clock64() : 0ull;
+        bool start = false;
+        if (pending) {
+            pending = false;
+            if (COUNT && wave_leader()) cnt.wadv++;
+            start = advance_lane<COUNT>(P, J, L, fr, T.found, T.best, cnt, job_cnt);
+        }
+        const bool idle = (L.job == -1);
+        const unsigned long long want = __ballot(idle);
+        if (want) {
+            if (lane_id == __ffsll((long long)want) - 1) s_base = atomicAdd(J.counter, __popcll(want));
+            __builtin_amdgcn_wave_barrier();
+            __syncthreads();
+            const int base = s_base;
+            if (idle) {
+                const int job = base + __popcll(want & ((1ull << lane_id) - 1ull));
+                if (job < J.njobs) {
+                    L.job = job;
+                    L.sample = 0;
+                    L.pacc = v3{0.0f, 0.0f, 0.0f};
+                    job_cnt.rays = 0u;
+                    if (J.mode == 0) {
+                        if (!job_pixel(P, job, L)) {
+                            L.job = -1;  // padding pixel: nothing to do, fetch again next round
+                        } else {
+                            L.nsamples = P.aa ? 4 : (P.multi ? P.sample_size : 1);
+                            queue_camera(P, L);
+                            start = true;
+                            if (P.pre_rec) {
+                                const int r = P.pre_rec[job];
+                                if (r != RT_PRE_NONE) {  // primary hit known: straight to phase A
+                                    start = false;
+                                    T.found = (r != RT_NO_HIT);
+                                    T.best.t = P.pre_t[job];
+                                    T.best.rec = r;
+                                    T.best.key = 0;
+                                    pending = true;
+                                }
+                            }
+                        }
+                    } else {
+                        const rt_ray r = J.rays[job];
+                        L.nsamples = 1;
+                        L.qo = v3{r.origin[0], r.origin[1], r.origin[2]};
+                        L.qd = v3{r.direction[0], r.direction[1], r.direction[2]};
+                        L.qt = r.t;
+                        L.qtype = Q_PATH;
+                        L.level = 0;
+                        start = true;
+                    }
+                } else {
+                    L.job = -2;  // no more work for this lane
+                }
+            }
+            __syncthreads();
+        }
+        if (start) {
+            cnt.rays++;
+            job_cnt.rays++;
+            trav_init(P, L, T);
+            tracing = true;
+        }
+        if (!__any(tracing)) {
+            if (!__any(L.job == -1 || pending)) break;  // every lane exhausted
+            continue;
+        }
+        // ---- phase B: node visits with postponed leaves (while-while), until enough lanes
+        // wait for phase A ----
+        unsigned long long tB = 0ull;
+        if (COUNT) {
+            tB = (unsigned long long)clock64();
+            cnt.cyc_a += tB - tA;
+        }
+        float4 g[8];
+        if (tracing && T.cur != RT_TRAV_NONE) node_fetch(S.nodes, T.cur, g);
+        for (;;) {
+            if (leaf_batch == 0) {
+                // if-if: every tracing lane takes one step per iteration, a leaf record if it
+                // has postponed ones, else a node visit
+                if (tracing) {
+                    if (leaf_pending(T))
+                        trav_record<COUNT>(S, T, cnt);
+                    else if (T.cur != RT_TRAV_NONE)
+                        trav_node<COUNT, BW>(S, T, stk, g, cnt);
+                }
+                if (tracing && !leaf_pending(T) && T.cur == RT_TRAV_NONE) {
+                    trav_finish(S, T);
+                    tracing = false;
+                    pending = true;
+                }
+                if (!__any(tracing)) break;
+                if (__popcll(__ballot(pending || L.job == -1)) >= refill_at) break;
+                continue;
+            }
+            const bool visit = tracing && !leaf_pending(T) && T.cur != RT_TRAV_NONE;
+            if (visit) trav_node<COUNT, BW>(S, T, stk, g, cnt);
+            // the leaf phase runs once no lane can visit a node without first testing its
+            // postponed leaves, or once `leaf_batch` lanes have some
+            const bool lp = tracing && leaf_pending(T);
+            const bool more_nodes = __any(tracing && !leaf_pending(T) && T.cur != RT_TRAV_NONE);
+            if (__any(lp) && (!more_nodes || __popcll(__ballot(lp)) >= leaf_batch)) {
+                bool work = lp;
+                while (__any(work)) {
+                    if (work) {
+                        trav_record<COUNT>(S, T, cnt);
+                        work = leaf_pending(T);
+                    }
+                }
+            }
+            if (tracing && !leaf_pending(T) && T.cur == RT_TRAV_NONE) {
+                trav_finish(S, T);
+                tracing = false;
+                pending = true;
+            }
+            if (!__any(tracing)) break;
+            if (__popcll(__ballot(pending || L.job == -1)) >= refill_at) break;
+        }
+        if (COUNT) cnt.cyc_b += (unsigned long long)clock64() - tB;
     }
     flush_counters<COUNT>(P, cnt);
 }

@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -16,6 +17,8 @@
 #include "rt_internal.h"
 #include "rt_kernels.hip"
 #include "rt_megakernel.hip"
+#include "rt_wavefront.hip"
+#include "rt_packet.hip"
 
 using namespace rt;
 
@@ -37,13 +40,28 @@ struct rt_ctx {
     int bvh_depth = 0;
     bool glossy_material = false;  // opaque, ks > 0, shininess != 0 (glossy_ray_count > 1 would call rand())
     int persistent_blocks[5] = {0, 0, 0, 0, 0};  // resident 64-lane blocks per WPE variant
+    // wavefront path (rt_wavefront.hip): queues, path state, frames, counters
+    float* d_wf_st = nullptr;  // 2 x WF_NFIELDS x cap
+    size_t wf_st_bytes = 0;
+    float* d_wf_res = nullptr;  // res_t[cap] | res_rec[cap]
+    size_t wf_res_bytes = 0;
+    float* d_wf_frames = nullptr;
+    size_t wf_frames_bytes = 0;
+    int* d_wf_cnt = nullptr;  // n[0], n[1], head, pad
+    int* h_wf_cnt = nullptr;  // pinned readback
+    int wf_trace_blocks[5] = {0, 0, 0, 0, 0};
+    std::vector<hipEvent_t> wf_ev;  // trace-launch event pairs
+    // primary packet pass (rt_packet.hip): per-job primary hit
+    float* d_pre = nullptr;  // pre_t[njobs] | pre_rec[njobs]
+    size_t pre_bytes = 0;
+    int bvh8_depth = 0;
 };
 
 // waves per SIMD the persistent kernel is compiled for (register cap); RT_WPE overrides for A/B runs
 static int wpe() {
     const char* w = std::getenv("RT_WPE");
     const int v = w ? std::atoi(w) : 2;
-    return (v == 1) ? 1 : 2;
+    return (v == 1 || v == 3 || v == 4) ? v : 2;
 }
 
 // BVH the persistent kernel walks, read once at rt_create: 8 (quantised 8-wide, default),
@@ -54,8 +72,46 @@ static int bvh_width_env() {
     return (v == 2 || v == 4) ? v : 8;
 }
 
+// RT_KERNEL: "tile" (rt_kernels.hip render_kernel), "persistent" (whole-traversal refill),
+// default: the dynamic-fetch persistent kernel (per-node-visit refill)
+// Default (no RT_KERNEL): whole-traversal refill for small scenes, where a query is a handful of
+// node visits and the per-step refill bookkeeping does not pay; dynamic fetch for large ones
+// (measured on MI355X, DESIGN.md section 6: C1/C2/C5 vs C3/C4).
+static bool use_whole_traversal_kernel(int ntri) {
+    const char* k = std::getenv("RT_KERNEL");
+    if (k && std::strcmp(k, "persistent") == 0) return true;
+    if (k && std::strcmp(k, "df") == 0) return false;
+    return ntri < 65536;
+}
+
+// waiting lanes that end a traversal phase of the dynamic-fetch kernel; RT_REFILL overrides
+static int refill_threshold() {
+    const char* r = std::getenv("RT_REFILL");
+    const int v = r ? std::atoi(r) : 16;
+    return std::min(64, std::max(1, v));
+}
+
+// lanes with postponed leaf records that start a leaf phase (64: only when no lane can visit a
+// node); RT_LEAFBATCH overrides
+static int leaf_batch_threshold() {
+    const char* r = std::getenv("RT_LEAFBATCH");
+    const int v = r ? std::atoi(r) : 0;
+    return std::min(64, std::max(0, v));  // 0: if-if (one leaf record or node visit per iteration)
+}
+
 template <bool COUNT, int BW>
 static void launch_wide(int grid, hipStream_t st, const KParams& K, const JobSrc& J) {
+    if (!use_whole_traversal_kernel(K.S.ntri)) {
+        if (wpe() == 1)
+            hipLaunchKernelGGL((persistent_df_kernel<COUNT, 1, BW>), dim3(grid), dim3(64), 0, st, K, J);
+        else if (wpe() == 4)
+            hipLaunchKernelGGL((persistent_df_kernel<COUNT, 4, BW>), dim3(grid), dim3(64), 0, st, K, J);
+        else if (wpe() == 3)
+            hipLaunchKernelGGL((persistent_df_kernel<COUNT, 3, BW>), dim3(grid), dim3(64), 0, st, K, J);
+        else
+            hipLaunchKernelGGL((persistent_df_kernel<COUNT, 2, BW>), dim3(grid), dim3(64), 0, st, K, J);
+        return;
+    }
     if (wpe() == 1)
         hipLaunchKernelGGL((persistent_kernel<COUNT, 1, BW>), dim3(grid), dim3(64), 0, st, K, J);
     else
@@ -90,9 +146,13 @@ static int persistent_grid(rt_ctx* c) {
     hipError_t e = hipErrorInvalidValue;
     // every BVH width compiles to the same LDS footprint and register cap per WPE
     if (wpe() == 1)
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_kernel<false, 1, 8>, 64, 0);
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_df_kernel<false, 1, 8>, 64, 0);
+    else if (wpe() == 3)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_df_kernel<false, 3, 8>, 64, 0);
+    else if (wpe() == 4)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_df_kernel<false, 4, 8>, 64, 0);
     else
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_kernel<false, 2, 8>, 64, 0);
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_df_kernel<false, 2, 8>, 64, 0);
     if (e != hipSuccess || per_cu <= 0) per_cu = 8;
     c->persistent_blocks[wpe()] = std::max(1, cus) * per_cu;
     return c->persistent_blocks[wpe()];
@@ -143,6 +203,13 @@ extern "C" int rt_destroy(rt_ctx* c) {
     if (c->d_img) hipFree(c->d_img);
     if (c->ev0) hipEventDestroy(c->ev0);
     if (c->ev1) hipEventDestroy(c->ev1);
+    if (c->d_wf_st) hipFree(c->d_wf_st);
+    if (c->d_wf_res) hipFree(c->d_wf_res);
+    if (c->d_wf_frames) hipFree(c->d_wf_frames);
+    if (c->d_wf_cnt) hipFree(c->d_wf_cnt);
+    if (c->d_pre) hipFree(c->d_pre);
+    if (c->h_wf_cnt) hipHostFree(c->h_wf_cnt);
+    for (hipEvent_t e : c->wf_ev) hipEventDestroy(e);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
     return RT_OK;
@@ -257,6 +324,7 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
         delete c;
         return RT_ERR_INVALID;
     }
+    c->bvh8_depth = bvh8.max_depth;
     if (c->bw > 2 && (bvh8.max_depth + 2 >= RT_STACK_SIZE || (int)bvh8.order.size() != ntri)) {
         set_error("rt_create: BVH8 deeper than the traversal stack");
         delete c;
@@ -429,6 +497,8 @@ static int fill_params(rt_ctx* c, const rt_camera* cam, const rt_params* p, int 
     K.aa_offx = 1.0f / (float)W * 0.25f;
     K.aa_offy = 1.0f / (float)H * 0.25f;
     K.stats = c->d_stats;
+    K.refill = refill_threshold();
+    K.leaf_batch = leaf_batch_threshold();
     return RT_OK;
 }
 
@@ -442,14 +512,243 @@ static int ensure(rt_ctx* c, float** buf, size_t* cap, size_t bytes) {
     return RT_OK;
 }
 
+// ---- wavefront path -------------------------------------------------------------------------
+static bool use_wavefront() {
+    const char* k = std::getenv("RT_KERNEL");
+    return k && std::strcmp(k, "wavefront") == 0;
+}
+
+static int wf_env(const char* name, int dflt, int lo, int hi) {
+    const char* v = std::getenv(name);
+    const int x = v ? std::atoi(v) : dflt;
+    return std::min(hi, std::max(lo, x));
+}
+
+static bool wf_debug() {
+    const char* v = std::getenv("RT_WF_DEBUG");
+    return v && v[0] == '1';
+}
+
+// trace-kernel waves per SIMD (register cap); RT_WF_WPE overrides for A/B runs
+static int wf_wpe() {
+    const int v = wf_env("RT_WF_WPE", 4, 2, 8);
+    return (v >= 8) ? 8 : (v >= 6) ? 6 : (v >= 4) ? 4 : 2;
+}
+
+template <bool COUNT, int BW>
+static void wf_launch_trace(int grid, hipStream_t st, const KParams& K, const WfBufs& W) {
+    switch (wf_wpe()) {
+        case 8: hipLaunchKernelGGL((wf_trace_kernel<COUNT, 8, BW>), dim3(grid), dim3(64), 0, st, K, W); break;
+        case 6: hipLaunchKernelGGL((wf_trace_kernel<COUNT, 6, BW>), dim3(grid), dim3(64), 0, st, K, W); break;
+        case 4: hipLaunchKernelGGL((wf_trace_kernel<COUNT, 4, BW>), dim3(grid), dim3(64), 0, st, K, W); break;
+        default: hipLaunchKernelGGL((wf_trace_kernel<COUNT, 2, BW>), dim3(grid), dim3(64), 0, st, K, W); break;
+    }
+}
+
+template <bool COUNT>
+static void wf_trace(const rt_ctx* c, int grid, hipStream_t st, KParams K, const WfBufs& W) {
+    K.S = c->S8;
+    if (c->bw == 4)
+        wf_launch_trace<COUNT, 4>(grid, st, K, W);
+    else
+        wf_launch_trace<COUNT, 8>(grid, st, K, W);
+}
+
+static int wf_trace_grid(rt_ctx* c) {
+    const int w = wf_wpe();
+    const int slot = (w == 8) ? 4 : (w == 6) ? 3 : (w == 4) ? 2 : 1;
+    if (c->wf_trace_blocks[slot] > 0) return c->wf_trace_blocks[slot];
+    int cus = 0, per_cu = 0;
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
+    hipError_t e;
+    switch (w) {
+        case 8: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wf_trace_kernel<false, 8, 8>, 64, 0); break;
+        case 6: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wf_trace_kernel<false, 6, 8>, 64, 0); break;
+        case 4: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wf_trace_kernel<false, 4, 8>, 64, 0); break;
+        default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wf_trace_kernel<false, 2, 8>, 64, 0); break;
+    }
+    if (e != hipSuccess || per_cu <= 0) per_cu = 4 * w;
+    c->wf_trace_blocks[slot] = std::max(1, cus) * per_cu;
+    return c->wf_trace_blocks[slot];
+}
+
+// One frame (or one rt_shade batch) as seed -> (trace -> shade)* iterations until every
+// sub-queue is empty.  The lengths live on the device; the host checks their sum every `batch`
+// iterations (kernels of an empty queue return at once).  trace_ms sums the trace launches.
+static int launch_wavefront(rt_ctx* c, const KParams& K0, const JobSrc& J, hipStream_t st, int count_mode,
+                            float* trace_ms, int* trace_launches) {
+    KParams K = K0;
+    K.S = c->S8;  // records are addressed in the wide BVH's leaf order by trace and shade alike
+    const int njobs = J.njobs;
+    if (njobs <= 0) return RT_OK;
+    if (c->bw <= 2) {
+        set_error("wavefront path needs the wide BVH (RT_BVH=4 or 8)");
+        return RT_ERR_INVALID;
+    }
+    const int nchunks = (njobs + 63) / 64;
+    const int seg = ((nchunks + WF_NQ - 1) / WF_NQ) * 64;
+    const int cap = seg * WF_NQ;
+    const int fpj = std::max(1, K.max_level);
+    int rc = ensure(c, &c->d_wf_st, &c->wf_st_bytes, (size_t)2 * WF_NFIELDS * cap * sizeof(float));
+    if (rc != RT_OK) return rc;
+    rc = ensure(c, &c->d_wf_res, &c->wf_res_bytes, (size_t)2 * cap * sizeof(float));
+    if (rc != RT_OK) return rc;
+    rc = ensure(c, &c->d_wf_frames, &c->wf_frames_bytes, (size_t)njobs * fpj * sizeof(Frame));
+    if (rc != RT_OK) return rc;
+    const size_t cnt_ints = (size_t)WF_C_KINDS * WF_NQ * WF_CSTRIDE + 64;
+    if (!c->d_wf_cnt) HIP_TRY(hipMalloc((void**)&c->d_wf_cnt, cnt_ints * sizeof(int)));
+    if (!c->h_wf_cnt) HIP_TRY(hipHostMalloc((void**)&c->h_wf_cnt, WF_NQ * sizeof(int)));
+    int* cn[2] = {c->d_wf_cnt + (size_t)WF_C_N0 * WF_NQ * WF_CSTRIDE, c->d_wf_cnt + (size_t)WF_C_N1 * WF_NQ * WF_CSTRIDE};
+    int* chead = c->d_wf_cnt + (size_t)WF_C_HEAD * WF_NQ * WF_CSTRIDE;
+    int* crays = c->d_wf_cnt + (size_t)WF_C_RAYS * WF_NQ * WF_CSTRIDE;
+    int* ctotal = c->d_wf_cnt + (size_t)WF_C_KINDS * WF_NQ * WF_CSTRIDE;
+    int cus = 0;
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
+    // both grids are multiples of WF_NQ (block b serves sub-queue b % WF_NQ)
+    int tgrid = std::max(WF_NQ, (wf_trace_grid(c) / WF_NQ) * WF_NQ);
+    if (const char* g = std::getenv("RT_WF_TGRID")) tgrid = std::max(WF_NQ, (std::atoi(g) / WF_NQ) * WF_NQ);
+    const int sgrid = std::max(WF_NQ, (std::max(1, cus) * 8 / WF_NQ) * WF_NQ);
+    float* st0 = c->d_wf_st;
+    float* st1 = c->d_wf_st + (size_t)WF_NFIELDS * cap;
+    WfBufs W{};
+    W.cap = cap;
+    W.seg = seg;
+    W.res_t = c->d_wf_res;
+    W.res_rec = reinterpret_cast<int*>(c->d_wf_res + cap);
+    W.frames = reinterpret_cast<Frame*>(c->d_wf_frames);
+    W.fpj = fpj;
+    W.refill = wf_env("RT_WF_REFILL", 8, 1, 64);
+    W.leaf_batch = wf_env("RT_WF_LEAFBATCH", 0, 0, 64);
+    W.head = chead;
+    W.rays = crays;
+    // seed -> queue 0; sub-queue q holds the jobs of chunks q, q + WF_NQ, ...
+    HIP_TRY(hipMemsetAsync(c->d_wf_cnt, 0, cnt_ints * sizeof(int), st));
+    hipLaunchKernelGGL(wf_seed_counts_kernel, dim3(1), dim3(WF_NQ), 0, st, cn[0], njobs);
+    W.st_out = st0;
+    const int seed_grid = (int)std::min<long long>(((long long)njobs + 63) / 64, (long long)std::max(1, cus) * 16);
+    hipLaunchKernelGGL(wf_seed_kernel, dim3(seed_grid), dim3(64), 0, st, K, J, W);
+    HIP_TRY(hipGetLastError());
+    const int batch = wf_env("RT_WF_BATCH", 4, 1, 64);
+    const bool timed = (trace_ms != nullptr);
+    int cur = 0, launches = 0;
+    std::vector<std::pair<int, int>> evs;  // event indices per trace launch
+    for (int iter = 0;;) {
+        for (int b = 0; b < batch; ++b, ++iter) {
+            const int out = 1 - cur;
+            W.st_in = cur ? st1 : st0;
+            W.n_in = cn[cur];
+            W.st_out = out ? st1 : st0;
+            W.n_out = cn[out];
+            hipLaunchKernelGGL(wf_reset_kernel, dim3(1), dim3(WF_NQ), 0, st, W.n_out, W.head);
+            if (timed) {
+                const size_t need = 2 * (evs.size() + 1);
+                while (c->wf_ev.size() < need) {
+                    hipEvent_t e;
+                    HIP_TRY(hipEventCreate(&e));
+                    c->wf_ev.push_back(e);
+                }
+                const int e0 = (int)(2 * evs.size());
+                evs.push_back({e0, e0 + 1});
+                HIP_TRY(hipEventRecord(c->wf_ev[e0], st));
+            }
+            if (count_mode)
+                wf_trace<true>(c, tgrid, st, K, W);
+            else
+                wf_trace<false>(c, tgrid, st, K, W);
+            if (timed) HIP_TRY(hipEventRecord(c->wf_ev[evs.back().second], st));
+            ++launches;
+            if (count_mode)
+                hipLaunchKernelGGL(wf_shade_kernel<true>, dim3(sgrid), dim3(64), 0, st, K, J, W);
+            else
+                hipLaunchKernelGGL(wf_shade_kernel<false>, dim3(sgrid), dim3(64), 0, st, K, J, W);
+            HIP_TRY(hipGetLastError());
+            cur = out;
+            if (wf_debug()) {  // RT_WF_DEBUG=1: per-iteration queue length and trace time (synchronous)
+                hipLaunchKernelGGL(wf_total_kernel, dim3(1), dim3(WF_NQ), 0, st, W.n_in, ctotal);
+                HIP_TRY(hipMemcpyAsync(c->h_wf_cnt, ctotal, sizeof(int), hipMemcpyDeviceToHost, st));
+                HIP_TRY(hipStreamSynchronize(st));
+                float ms = 0.0f;
+                if (timed) hipEventElapsedTime(&ms, c->wf_ev[evs.back().first], c->wf_ev[evs.back().second]);
+                std::fprintf(stderr, "wf iter %d: queries %d trace %.3f ms\n", iter, c->h_wf_cnt[0], ms);
+            }
+        }
+        hipLaunchKernelGGL(wf_total_kernel, dim3(1), dim3(WF_NQ), 0, st, cn[cur], ctotal);
+        HIP_TRY(hipMemcpyAsync(c->h_wf_cnt, ctotal, sizeof(int), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        if (c->h_wf_cnt[0] == 0) break;
+        if (iter > 1000000) {
+            set_error("wavefront: queue did not drain");
+            return RT_ERR_INVALID;
+        }
+    }
+    hipLaunchKernelGGL(wf_finish_kernel, dim3(1), dim3(WF_NQ), 0, st, crays, c->d_stats);
+    HIP_TRY(hipGetLastError());
+    if (timed) {
+        float tot = 0.0f;
+        for (auto& e : evs) {
+            float ms = 0.0f;
+            HIP_TRY(hipEventElapsedTime(&ms, c->wf_ev[e.first], c->wf_ev[e.second]));
+            tot += ms;
+        }
+        *trace_ms = tot;
+    }
+    if (trace_launches) *trace_launches = launches;
+    return RT_OK;
+}
+
+// primary packet pass (rt_packet.hip) ahead of the megakernels; RT_PACKET=0 disables it
+static bool use_packets(const rt_ctx* c, const KParams& K) {
+    const char* v = std::getenv("RT_PACKET");
+    if (!v || v[0] != '1') return false;  // opt-in: measured slower than the megakernels' own primaries
+    // one camera ray per pixel; the shared stack holds at most (width-1) entries per level
+    return c->bw > 2 && !K.aa && !K.multi && c->bvh8_depth * (c->bw - 1) + 2 <= PK_STACK;
+}
+
+static int launch_packets(rt_ctx* c, KParams& K, hipStream_t st, int count_mode, int njobs) {
+    int rc = ensure(c, &c->d_pre, &c->pre_bytes, (size_t)2 * njobs * sizeof(float));
+    if (rc != RT_OK) return rc;
+    K.pre_t = c->d_pre;
+    K.pre_rec = reinterpret_cast<const int*>(c->d_pre + njobs);
+    KParams Kp = K;
+    Kp.S = c->S8;
+    int cus = 0;
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
+    const int ntiles = (njobs + 63) / 64;
+    const int grid = std::min(ntiles, std::max(1, cus) * 16);
+    float* pt = c->d_pre;
+    int* pr = reinterpret_cast<int*>(c->d_pre + njobs);
+    if (c->bw == 4) {
+        if (count_mode)
+            hipLaunchKernelGGL((primary_packet_kernel<true, 4>), dim3(grid), dim3(64), 0, st, Kp, pt, pr, ntiles);
+        else
+            hipLaunchKernelGGL((primary_packet_kernel<false, 4>), dim3(grid), dim3(64), 0, st, Kp, pt, pr, ntiles);
+    } else {
+        if (count_mode)
+            hipLaunchKernelGGL((primary_packet_kernel<true, 8>), dim3(grid), dim3(64), 0, st, Kp, pt, pr, ntiles);
+        else
+            hipLaunchKernelGGL((primary_packet_kernel<false, 8>), dim3(grid), dim3(64), 0, st, Kp, pt, pr, ntiles);
+    }
+    HIP_TRY(hipGetLastError());
+    return RT_OK;
+}
+
 static int launch_render(rt_ctx* c, KParams& K, hipStream_t st, int count_mode, rt_stats* stats) {
     const int tiles_x = (K.W + 7) / 8;
     const int tiles_y = (K.band_rows + 7) / 8;
     const long long blocks = (long long)tiles_x * tiles_y * K.n_local_bands;
+    float trace_ms = 0.0f;
+    int trace_launches = 0;
     HIP_TRY(hipMemsetAsync(c->d_stats, 0, 16 * sizeof(unsigned long long), st));
     if (blocks > 0) {
         HIP_TRY(hipEventRecord(c->ev0, st));
-        if (use_tile_kernel()) {
+        if (use_wavefront() && c->bw > 2) {
+            JobSrc J{};
+            J.mode = 0;
+            J.njobs = (int)(blocks * 64);
+            int rc = launch_wavefront(c, K, J, st, count_mode, stats ? &trace_ms : nullptr,
+                                      stats ? &trace_launches : nullptr);
+            if (rc != RT_OK) return rc;
+        } else if (use_tile_kernel()) {
             if (count_mode)
                 hipLaunchKernelGGL(render_kernel<true>, dim3((unsigned)blocks), dim3(64), 0, st, K);
             else
@@ -459,6 +758,10 @@ static int launch_render(rt_ctx* c, KParams& K, hipStream_t st, int count_mode, 
             J.mode = 0;
             J.njobs = (int)(blocks * 64);
             J.counter = reinterpret_cast<int*>(c->d_stats + 7);
+            if (use_packets(c, K)) {
+                const int rc = launch_packets(c, K, st, count_mode, J.njobs);
+                if (rc != RT_OK) return rc;
+            }
             const int grid = (int)std::min<long long>(blocks, persistent_grid(c));
             if (count_mode)
                 launch_persistent<true>(grid, st, K, J, c);
@@ -479,6 +782,9 @@ static int launch_render(rt_ctx* c, KParams& K, hipStream_t st, int count_mode, 
         float ms = 0.0f;
         if (blocks > 0) HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
         stats->kernel_ms = ms;
+        stats->node_bytes = (use_tile_kernel() || c->bw == 2) ? 64u : 128u;
+        stats->trace_ms = trace_ms;
+        stats->trace_launches = (uint32_t)trace_launches;
     }
     return RT_OK;
 }
@@ -600,7 +906,22 @@ extern "C" int rt_shade(rt_ctx* c, const rt_ray* rays, int n, const rt_params* p
     HIP_TRY(hipMalloc(&d_c, sizeof(float) * 3 * n));
     HIP_TRY(hipMalloc(&d_n, sizeof(unsigned long long) * n));
     hipMemcpy(d_r, rays, sizeof(rt_ray) * n, hipMemcpyHostToDevice);
-    if (use_tile_kernel()) {
+    if (use_wavefront() && c->bw > 2) {
+        JobSrc J{};
+        J.mode = 1;
+        J.njobs = n;
+        J.rays = d_r;
+        J.rgb = d_c;
+        J.ray_counts = d_n;
+        hipMemsetAsync(c->d_stats, 0, 16 * sizeof(unsigned long long), c->stream);
+        const int rc = launch_wavefront(c, K, J, c->stream, 0, nullptr, nullptr);
+        if (rc != RT_OK) {
+            hipFree(d_r);
+            hipFree(d_c);
+            hipFree(d_n);
+            return rc;
+        }
+    } else if (use_tile_kernel()) {
         hipLaunchKernelGGL(shade_kernel, dim3((n + 63) / 64), dim3(64), 0, c->stream, K, d_r, n, d_c, d_n);
     } else {
         JobSrc J{};

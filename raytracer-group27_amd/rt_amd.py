@@ -85,7 +85,8 @@ class rt_hit(C.Structure):
 
 class rt_stats(C.Structure):
     _fields_ = [("rays", C.c_uint64), ("node_visits", C.c_uint64), ("tri_tests", C.c_uint64),
-                ("hits", C.c_uint64), ("kernel_ms", C.c_float), ("pad_", C.c_float)]
+                ("hits", C.c_uint64), ("kernel_ms", C.c_float), ("node_bytes", C.c_uint32),
+                ("trace_ms", C.c_float), ("trace_launches", C.c_uint32)]
 
 
 RAY_DTYPE = np.dtype([("origin", "<f4", 3), ("direction", "<f4", 3), ("t", "<f4")])

@@ -1,0 +1,33 @@
+"""Developer tool: SIMD efficiency of the persistent kernels from the counting build.
+Per config and variant: lane node visits / (64 x wave node steps), same for triangle records
+and for state-machine advances (one per query).  Usage: python tools/simd_eff.py C3 old:RT_KERNEL=persistent df:"""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "raytracer-group27_amd"))
+import rt_amd as R  # noqa: E402
+
+args = sys.argv[1:]
+cfgs = [a for a in args if a.startswith("C") and ":" not in a] or ["C3"]
+variants = [(a.split(":", 1)[0], dict(x.split("=") for x in a.split(":", 1)[1].split(",") if x))
+            for a in args if ":" in a] or [("default", {})]
+keys = set(k for _, e in variants for k in e)
+for cfg in cfgs:
+    s, p, W, H, desc = R.build_config(cfg)
+    ctx = R.Context(s)
+    cam = R.camera_from_trackball(aspect=R.aspect_of(W, H))
+    for name, env in variants:
+        for k in keys:
+            os.environ.pop(k, None)
+        os.environ.update(env)
+        R.set_counting(True)
+        _, st = ctx.render(cam, p, W, H)
+        R.set_counting(False)
+        c = ctx.debug_counters()
+        rays, nodes, tris, hits, wn, wt, wa = (int(x) for x in c[:7])
+        print(f"{cfg} {name}: rays={rays} nodes/ray={nodes / rays:.2f} tris/ray={tris / rays:.2f} "
+              f"eff_node={nodes / max(1, 64 * wn):.3f} eff_tri={tris / max(1, 64 * wt):.3f} "
+              f"eff_adv={rays / max(1, 64 * wa):.3f} wave_steps/ray: node={wn / rays:.3f} tri={wt / rays:.3f} "
+              f"adv={wa / rays:.3f} cycA={int(c[8]) / max(1, int(c[8]) + int(c[9])):.2f}", flush=True)
+    ctx.close()
