@@ -219,6 +219,44 @@ int rt_ctx_info(rt_ctx* ctx, int* num_nodes, int* num_tri_records, int* ref_bvh_
 /* Device math self-test: out[i] = {sqrtf(x), 1/x, x/y, powf(x,y)} bits for parity of the math lib. */
 int rt_selftest_math(rt_ctx* ctx, const float* x, const float* y, int n, float* out);
 
+/* ---- Screen post-processing (src/screen.cpp) ------------------------------------------------
+ * Settings of class Screen (src/screen.h:58-111), raw values as the GUI passes them to the
+ * setters; the setters' clamps (setKernelNumRepetitions >= 1, setSigma >= 0.001) are applied
+ * inside, and setFilterSize keeps the raw value (its clamp hits a local, src/screen.cpp:212-215).
+ * Images are W*H*3 floats in Screen::m_textureData order (top row first).                      */
+enum { RT_BLOOM_NONE = 0, RT_BLOOM = 1, RT_BLOOM_REINHARD = 2, RT_BLOOM_EXPOSURE = 3, RT_BLOOM_ONLY_LIGHT = 4,
+       RT_BLOOM_ONLY_LIGHT_KERNEL = 5 };                  /* enum class FilteringOption */
+enum { RT_KERNEL_BOX = 0, RT_KERNEL_GAUSSIAN = 1 };      /* enum class Kernel */
+typedef struct rt_post_params {
+    int filtering_option;   /* setBloomFilter */
+    int kernel;             /* setKernel */
+    int repetitions;        /* setKernelNumRepetitions (raw) */
+    int filter_size;        /* setFilterSize (raw) */
+    float sigma;            /* setSigma (raw) */
+    float exposure;         /* setExposure */
+    int gamma_correction;   /* enableGammaCorrection */
+    float gamma;            /* setGammaValue */
+    int bloom_live;         /* setBloomFilterLive */
+    int pad_;
+} rt_post_params;
+
+/* Screen::postprocessImage (src/screen.cpp:56-69): bloom if bloom_live, then gamma if enabled.
+ * d_rgb is read and written in place; d_scratch holds 2*W*H*3 floats (bloom temporaries). */
+int rt_postprocess_device(const rt_post_params* p, int width, int height, float* d_rgb, float* d_scratch,
+                          void* stream);
+/* Screen::writeBitmapToFile's pixel path (src/screen.cpp:40-54): applyBloomEffect on d_rgb (in
+ * place, as the reference mutates m_textureData), then clamp to [0,1] and truncate *255 into
+ * RGBA8 (alpha 255). */
+int rt_bitmap_device(const rt_post_params* p, int width, int height, float* d_rgb, float* d_scratch,
+                     uint8_t* d_rgba8, void* stream);
+/* Host-buffer forms of the two above (synchronous, device 0 of the caller's current device). */
+int rt_postprocess(const rt_post_params* p, int width, int height, float* rgb);
+int rt_bitmap(const rt_post_params* p, int width, int height, float* rgb, uint8_t* rgba8);
+/* stbi_write_bmp as the reference calls it (comp 4): 24-bit BMP, bottom-up rows, alpha dropped.
+ * rt_encode_bmp writes into out (size >= 54 + (3W + pad) * H) and returns the byte count. */
+long rt_encode_bmp(int width, int height, const uint8_t* rgba8, uint8_t* out, long out_size);
+int rt_write_bmp(const char* path, int width, int height, const uint8_t* rgba8);
+
 #ifdef __cplusplus
 }
 #endif

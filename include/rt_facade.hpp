@@ -220,5 +220,61 @@ inline void renderRayTracing(const Trackball& cam, const BoundingVolumeHierarchy
     check(rt_render(bvh.handle(), &c, &p, W, H, screen.data(), nullptr), "renderRayTracing");
 }
 
+// class Screen (src/screen.h:32-161): the framebuffer renderRayTracing fills, with the
+// reference's post-processing setters; postprocessImage / writeBitmapToFile run on the GPU
+// (rt_postprocess / rt_bitmap + rt_write_bmp).  The GL draw() path is out of scope.
+enum class FilteringOption { None, Bloom, BloomWithReinhardHdr, BloomWithExposureHdr, OnlyLight, OnlyLightWithKernel };
+enum class Kernel { BoxKernel, GaussianKernel };
+
+class Screen {
+public:
+    Screen(int width, int height) : W_(width), H_(height), data_((size_t)width * height * 3, 0.0f) {}
+    void clear(const vec3& c) {
+        for (size_t k = 0; k < data_.size(); k += 3) {
+            data_[k] = c.x;
+            data_[k + 1] = c.y;
+            data_[k + 2] = c.z;
+        }
+    }
+    void setPixel(int x, int y, const vec3& c) {  // (0,0) bottom left, stored top row first
+        const size_t i = ((size_t)(H_ - 1 - y) * W_ + x) * 3;
+        data_[i] = c.x;
+        data_[i + 1] = c.y;
+        data_[i + 2] = c.z;
+    }
+    void postprocessImage() { check(rt_postprocess(&p_, W_, H_, data_.data()), "postprocessImage"); }
+    void writeBitmapToFile(const std::string& path) {
+        std::vector<uint8_t> rgba((size_t)W_ * H_ * 4);
+        check(rt_bitmap(&p_, W_, H_, data_.data(), rgba.data()), "writeBitmapToFile");
+        check(rt_write_bmp(path.c_str(), W_, H_, rgba.data()), "writeBitmapToFile");
+    }
+    void setBloomFilterLive(bool v) { p_.bloom_live = v ? 1 : 0; }
+    void setBloomFilter(FilteringOption o) { p_.filtering_option = (int)o; }
+    void setKernel(Kernel k) { p_.kernel = (int)k; }
+    void setKernelNumRepetitions(int r) { p_.repetitions = r; }
+    void setGammaValue(float g) { p_.gamma = g; }
+    void enableGammaCorrection(float on) { p_.gamma_correction = on != 0.0f ? 1 : 0; }
+    void setSigma(float s) { p_.sigma = s; }
+    void setExposure(float e) { p_.exposure = e; }
+    void setFilterSize(int f) { p_.filter_size = f; }
+    std::vector<float>& textureData() { return data_; }
+    int width() const { return W_; }
+    int height() const { return H_; }
+
+private:
+    int W_, H_;
+    std::vector<float> data_;
+    rt_post_params p_{0, 0, 1, 5, 2.0f, 0.5f, 0, 2.2f, 0, 0};  // Screen's member defaults
+};
+
+// renderRayTracing into a Screen, then Screen::postprocessImage (src/main.cpp:398)
+inline void renderRayTracing(const Trackball& cam, const BoundingVolumeHierarchy& bvh, Screen& screen,
+                             bool anti_aliasing = false, bool multipleRays = false, int sampleSize = 4,
+                             const RenderSettings& s = {}) {
+    renderRayTracing(cam, bvh, screen.width(), screen.height(), screen.textureData(), anti_aliasing, multipleRays,
+                     sampleSize, s);
+    screen.postprocessImage();
+}
+
 }  // namespace facade
 }  // namespace rt

@@ -42,6 +42,8 @@ def lib():
         L.oracle_render.argtypes = [vp, F3, F3, C.c_float, C.c_float, C.c_int, C.c_int, vp, F3,
                                     C.POINTER(C.c_uint64)]
         L.oracle_set_threads.argtypes = [C.c_int]
+        L.oracle_postprocess.argtypes = [vp, C.c_int, C.c_int, F3]
+        L.oracle_bitmap.argtypes = [vp, C.c_int, C.c_int, F3, C.POINTER(C.c_uint8)]
         _lib = L
     return _lib
 
@@ -119,6 +121,21 @@ class Oracle:
         lib().oracle_render(self.h, _fp(la), _fp(eu), float(dist), float(fovy), W, H, C.addressof(prm), _fp(rgb),
                             C.byref(total))
         return rgb, total.value
+
+
+def postprocess(rgb, W, H, prm):
+    """Screen::postprocessImage restated on the CPU (ref_post.cpp); prm is an rt_post_params."""
+    out = np.ascontiguousarray(rgb, np.float32).copy()
+    lib().oracle_postprocess(C.addressof(prm), W, H, _fp(out))
+    return out
+
+
+def bitmap(rgb, W, H, prm):
+    """Screen::writeBitmapToFile's pixel path restated on the CPU: (bloomed floats, RGBA8)."""
+    out = np.ascontiguousarray(rgb, np.float32).copy()
+    rgba = np.zeros(W * H * 4, np.uint8)
+    lib().oracle_bitmap(C.addressof(prm), W, H, _fp(out), rgba.ctypes.data_as(C.POINTER(C.c_uint8)))
+    return out, rgba
 
 
 def set_threads(n):

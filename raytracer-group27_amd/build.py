@@ -12,8 +12,8 @@ CSRC = os.path.join(HERE, "csrc")
 BUILD = os.path.join(HERE, "build")
 LIB = os.path.join(HERE, "librt_amd.so")
 
-HOST_SRCS = ["obj_loader.cpp", "scene.cpp", "bvh_build.cpp", "rt_api_host.cpp"]
-HIP_SRCS = ["rt_runtime.hip"]
+HOST_SRCS = ["obj_loader.cpp", "scene.cpp", "bvh_build.cpp", "rt_api_host.cpp", "bmp.cpp"]
+HIP_SRCS = ["rt_runtime.hip", "rt_post.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("RT_OFFLOAD_ARCH", "gfx950")
 

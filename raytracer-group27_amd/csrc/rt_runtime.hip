@@ -531,15 +531,12 @@ static bool wf_debug() {
 
 // trace-kernel waves per SIMD (register cap); RT_WF_WPE overrides for A/B runs
 static int wf_wpe() {
-    const int v = wf_env("RT_WF_WPE", 4, 2, 8);
-    return (v >= 8) ? 8 : (v >= 6) ? 6 : (v >= 4) ? 4 : 2;
+    return wf_env("RT_WF_WPE", 4, 2, 4) >= 4 ? 4 : 2;  // 6 and 8 do not fit: the kernel needs ~105 VGPRs
 }
 
 template <bool COUNT, int BW>
 static void wf_launch_trace(int grid, hipStream_t st, const KParams& K, const WfBufs& W) {
     switch (wf_wpe()) {
-        case 8: hipLaunchKernelGGL((wf_trace_kernel<COUNT, 8, BW>), dim3(grid), dim3(64), 0, st, K, W); break;
-        case 6: hipLaunchKernelGGL((wf_trace_kernel<COUNT, 6, BW>), dim3(grid), dim3(64), 0, st, K, W); break;
         case 4: hipLaunchKernelGGL((wf_trace_kernel<COUNT, 4, BW>), dim3(grid), dim3(64), 0, st, K, W); break;
         default: hipLaunchKernelGGL((wf_trace_kernel<COUNT, 2, BW>), dim3(grid), dim3(64), 0, st, K, W); break;
     }
@@ -562,8 +559,6 @@ static int wf_trace_grid(rt_ctx* c) {
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
     hipError_t e;
     switch (w) {
-        case 8: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wf_trace_kernel<false, 8, 8>, 64, 0); break;
-        case 6: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wf_trace_kernel<false, 6, 8>, 64, 0); break;
         case 4: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wf_trace_kernel<false, 4, 8>, 64, 0); break;
         default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wf_trace_kernel<false, 2, 8>, 64, 0); break;
     }

@@ -102,7 +102,54 @@ EXPORTS = [
     "rt_scene_desc_get", "rt_scene_free", "rt_write_dragon_proxy", "rt_camera_from_trackball", "rt_create",
     "rt_destroy", "rt_render", "rt_render_device", "rt_unpermute_bands_device", "rt_intersect", "rt_shade",
     "rt_set_counting", "rt_debug_counters", "rt_ctx_info", "rt_selftest_math",
+    "rt_postprocess_device", "rt_bitmap_device", "rt_postprocess", "rt_bitmap", "rt_encode_bmp", "rt_write_bmp",
 ]
+
+class rt_post_params(C.Structure):
+    """Screen post-processing settings (src/screen.h:58-111), raw setter values."""
+    _fields_ = [("filtering_option", C.c_int), ("kernel", C.c_int), ("repetitions", C.c_int),
+                ("filter_size", C.c_int), ("sigma", C.c_float), ("exposure", C.c_float),
+                ("gamma_correction", C.c_int), ("gamma", C.c_float), ("bloom_live", C.c_int), ("pad_", C.c_int)]
+
+
+# FilteringOption / Kernel (src/screen.h:16-30)
+BLOOM_NONE, BLOOM, BLOOM_REINHARD, BLOOM_EXPOSURE, BLOOM_ONLY_LIGHT, BLOOM_ONLY_LIGHT_KERNEL = range(6)
+KERNEL_BOX, KERNEL_GAUSSIAN = 0, 1
+
+
+def post_params(filtering_option=BLOOM_NONE, kernel=KERNEL_BOX, repetitions=1, filter_size=5, sigma=2.0,
+                exposure=0.5, gamma_correction=False, gamma=2.2, bloom_live=False):
+    """Defaults of class Screen and of main.cpp's bloom settings (src/main.cpp:426-435)."""
+    return rt_post_params(int(filtering_option), int(kernel), int(repetitions), int(filter_size), float(sigma),
+                          float(exposure), int(bool(gamma_correction)), float(gamma), int(bool(bloom_live)), 0)
+
+
+def postprocess(rgb, W, H, prm):
+    """Screen::postprocessImage on a host image (W*H*3 float32, setPixel order); returns a copy."""
+    out = np.ascontiguousarray(rgb, np.float32).copy()
+    check(lib().rt_postprocess(C.byref(prm), W, H, out.ctypes.data_as(C.POINTER(C.c_float))), "rt_postprocess")
+    return out
+
+
+def bitmap(rgb, W, H, prm):
+    """Screen::writeBitmapToFile's pixel path: (bloomed float image, RGBA8 [H*W*4])."""
+    out = np.ascontiguousarray(rgb, np.float32).copy()
+    rgba = np.zeros(W * H * 4, np.uint8)
+    check(lib().rt_bitmap(C.byref(prm), W, H, out.ctypes.data_as(C.POINTER(C.c_float)),
+                          rgba.ctypes.data_as(C.POINTER(C.c_uint8))), "rt_bitmap")
+    return out, rgba
+
+
+def encode_bmp(rgba, W, H):
+    """stbi_write_bmp bytes of an RGBA8 image (24-bit, bottom-up, alpha dropped)."""
+    rgba = np.ascontiguousarray(rgba, np.uint8)
+    size = 54 + (3 * W + ((-3 * W) & 3)) * H
+    buf = np.zeros(size, np.uint8)
+    n = lib().rt_encode_bmp(W, H, rgba.ctypes.data_as(C.POINTER(C.c_uint8)), buf.ctypes.data_as(C.POINTER(C.c_uint8)),
+                            size)
+    check(int(n) if n < 0 else 0, "rt_encode_bmp")
+    return buf[:n].tobytes()
+
 
 _lib = None
 
@@ -146,6 +193,12 @@ def lib():
             "rt_debug_counters": ([vp, P(C.c_uint64), C.c_int], C.c_int),
             "rt_ctx_info": ([vp, P(C.c_int), P(C.c_int), P(C.c_int), P(C.c_int)], C.c_int),
             "rt_selftest_math": ([vp, P(C.c_float), P(C.c_float), C.c_int, P(C.c_float)], C.c_int),
+            "rt_postprocess_device": ([P(rt_post_params), C.c_int, C.c_int, vp, vp, vp], C.c_int),
+            "rt_bitmap_device": ([P(rt_post_params), C.c_int, C.c_int, vp, vp, vp, vp], C.c_int),
+            "rt_postprocess": ([P(rt_post_params), C.c_int, C.c_int, P(C.c_float)], C.c_int),
+            "rt_bitmap": ([P(rt_post_params), C.c_int, C.c_int, P(C.c_float), P(C.c_uint8)], C.c_int),
+            "rt_encode_bmp": ([C.c_int, C.c_int, P(C.c_uint8), P(C.c_uint8), C.c_long], C.c_long),
+            "rt_write_bmp": ([C.c_char_p, C.c_int, C.c_int, P(C.c_uint8)], C.c_int),
         }
         for name, (args, res) in sigs.items():
             f = getattr(L, name)

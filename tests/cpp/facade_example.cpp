@@ -27,6 +27,16 @@ int main(int argc, char** argv) {
         double sum = 0;
         for (float v : screen) sum += v;
         std::printf("frame_sum=%.9g\n", sum);
+        // Screen + bloom + gamma + BMP, as the "Render to file" button does (src/main.cpp:513-522)
+        Screen scr(32, 24);
+        scr.setBloomFilter(FilteringOption::BloomWithReinhardHdr);
+        scr.setKernel(Kernel::GaussianKernel);
+        scr.setFilterSize(2);
+        scr.enableGammaCorrection(true);
+        renderRayTracing(Trackball{}, bvh, scr);
+        const char* out = argc > 2 ? argv[2] : "facade_render.bmp";
+        scr.writeBitmapToFile(out);
+        std::printf("bmp=%s\n", out);
         return h ? 0 : 5;
     } catch (const std::exception& e) {
         std::printf("no device: %s\n", e.what());

@@ -31,6 +31,9 @@ def test_facade_builds_and_fails_loudly_without_gpu(R, tmp_path):
 @pytest.mark.gpu
 def test_facade_runs_on_gpu(R, tmp_path):
     exe = build_example(tmp_path)
-    r = subprocess.run([exe, R.data_dir()], capture_output=True, text=True)
+    bmp = str(tmp_path / "render.bmp")
+    r = subprocess.run([exe, R.data_dir(), bmp], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "hit=1" in r.stdout and "frame_sum=" in r.stdout
+    data = open(bmp, "rb").read()
+    assert data[:2] == b"BM" and len(data) == 54 + 32 * 3 * 24

@@ -179,3 +179,45 @@ def test_invalid_params_fail_loudly(R, ctxs):
     bad = R.params(max_reflection_level=99, glossy_ray_count=1)
     with pytest.raises(R.RtError, match="max_reflection_level"):
         ctx.render(R.camera_from_trackball(), bad, 8, 8)
+
+
+KERNEL_VARIANTS = [
+    {"RT_KERNEL": "persistent"},
+    {"RT_KERNEL": "df"},
+    {"RT_KERNEL": "df", "RT_LEAFBATCH": "64"},
+    {"RT_KERNEL": "wavefront"},
+    {"RT_KERNEL": "tile"},
+    {"RT_KERNEL": "persistent", "RT_PACKET": "1"},
+    {"RT_KERNEL": "df", "RT_PACKET": "1"},
+]
+
+
+@pytest.mark.parametrize("case", ["c2_64x48", "c3s_96x54", "c4s_64x36", "c5_96x54", "c5_depth3_bvh_64x36"])
+def test_kernel_variants_bit_identical(R, ctxs, golden_dir, case):
+    """Every render path (whole-traversal / dynamic-fetch megakernels, wavefront queues, tile
+    kernel, primary packets) gives the same bits and ray count, and matches the golden image."""
+    name, cfg, W, H, uv, over = next(c for c in IMAGES if c[0] == case)
+    g = golden(golden_dir)[name]
+    _, ctx, prm, _, _ = ctxs(cfg, uv)
+    prm = apply(R.rt_params.from_buffer_copy(prm), over)
+    cam = R.camera_from_trackball(aspect=R.aspect_of(W, H))
+    keys = {k for v in KERNEL_VARIANTS for k in v}
+    saved = {k: os.environ.get(k) for k in keys}
+    try:
+        base = None
+        for v in KERNEL_VARIANTS:
+            for k in keys:
+                os.environ.pop(k, None)
+            os.environ.update(v)
+            img, st = ctx.render(cam, prm, W, H)
+            assert st.rays == int(g["rays"]), v
+            assert float(np.max(np.abs(img - g["img"]))) <= TOL, v
+            if base is None:
+                base = img
+            assert img.tobytes() == base.tobytes(), v
+    finally:
+        for k, val in saved.items():
+            if val is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = val
