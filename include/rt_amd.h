@@ -219,6 +219,10 @@ int rt_ctx_info(rt_ctx* ctx, int* num_nodes, int* num_tri_records, int* ref_bvh_
 /* Device math self-test: out[i] = {sqrtf(x), 1/x, x/y, powf(x,y)} bits for parity of the math lib. */
 int rt_selftest_math(rt_ctx* ctx, const float* x, const float* y, int n, float* out);
 
+/* Philox-4x32-10 (the glossy-lobe stream that replaces rand(), src/main.cpp:234-235): the same
+ * host/device function the kernels call, exported for known-answer tests. */
+int rt_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+
 /* ---- Screen post-processing (src/screen.cpp) ------------------------------------------------
  * Settings of class Screen (src/screen.h:58-111), raw values as the GUI passes them to the
  * setters; the setters' clamps (setKernelNumRepetitions >= 1, setSigma >= 0.001) are applied

@@ -42,6 +42,8 @@ def lib():
         L.oracle_render.argtypes = [vp, F3, F3, C.c_float, C.c_float, C.c_int, C.c_int, vp, F3,
                                     C.POINTER(C.c_uint64)]
         L.oracle_set_threads.argtypes = [C.c_int]
+        U3 = C.POINTER(C.c_uint32)
+        L.oracle_philox.argtypes = [U3, U3, U3]
         L.oracle_postprocess.argtypes = [vp, C.c_int, C.c_int, F3]
         L.oracle_bitmap.argtypes = [vp, C.c_int, C.c_int, F3, C.POINTER(C.c_uint8)]
         _lib = L

@@ -360,7 +360,35 @@ static bool walk_bvh(const Scene& sc, int ni, Ray& r, Hit& h) {
 
 struct Counter {
     uint64_t rays = 0;
+    // glossy lobes: rand() replaced by a Philox-4x32-10 stream, counter (draw, pixel, sample, 0)
+    uint32_t pix = 0, sample = 0, draws = 0;
 };
+
+// Philox-4x32-10 (Salmon, Moraes, Dror, Shaw, SC'11), Random123's round constants and key bumps.
+static void philox(uint32_t ctr[4], uint64_t seed) {
+    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    for (int round = 0; round < 10; ++round) {
+        if (round) {
+            k0 += 0x9E3779B9u;
+            k1 += 0xBB67AE85u;
+        }
+        const uint64_t m0 = (uint64_t)ctr[0] * 0xD2511F53u, m1 = (uint64_t)ctr[2] * 0xCD9E8D57u;
+        const uint32_t x0 = (uint32_t)(m1 >> 32) ^ ctr[1] ^ k0, x1 = (uint32_t)m1;
+        const uint32_t x2 = (uint32_t)(m0 >> 32) ^ ctr[3] ^ k1, x3 = (uint32_t)m0;
+        ctr[0] = x0;
+        ctr[1] = x1;
+        ctr[2] = x2;
+        ctr[3] = x3;
+    }
+}
+
+// two uniforms in [0,1) (top 24 bits) per draw, in place of rand() / (float)RAND_MAX
+static void draw_pair(Counter& cnt, uint64_t seed, float& a, float& b) {
+    uint32_t c[4] = {cnt.draws++, cnt.pix, cnt.sample, 0u};
+    philox(c, seed);
+    a = (float)(c[0] >> 8) / 16777216.0f;
+    b = (float)(c[1] >> 8) / 16777216.0f;
+}
 
 static bool intersect(const Scene& sc, Ray& r, Hit& h, bool use_bvh, Counter& cnt) {
     cnt.rays++;
@@ -541,7 +569,39 @@ static V3 final_color(Scene& sc, const rt_params& P, Ray ray, int level, Counter
             rr.direction = refl;
             mirror += m.ks * final_color(sc, P, rr, level + 1, cnt);
             if (m.shininess != 0) {
-                // glossy_ray_count > 1 draws rand() here (main.cpp:227-249); not restated.
+                // glossy lobe (main.cpp:209-250); rand() pairs come from the Philox stream
+                V3 notr = refl;
+                if (refl.x != 0) {
+                    notr.y = -refl.x;
+                    notr.x = refl.y;
+                } else {
+                    notr.y = -refl.z;
+                    notr.z = refl.y;
+                }
+                const V3 pr1 = vcross(refl, notr);
+                const V3 pr2 = vcross(refl, pr1);
+                const float s = m.shininess;
+                const float d = std::pow(0.5f, -1 / s) * std::sqrt(1 - std::pow(0.5, 2 / s));
+                for (int i = 1; i < P.glossy_ray_count; i++) {
+                    V3 dir;
+                    float a, b;
+                    int loops = 0;
+                    do {
+                        do {
+                            draw_pair(cnt, P.rng_seed, a, b);
+                        } while (a == 0 && b == 0 && a * a + b * b < 1);
+                        a = (2 * a - 1) * d;
+                        b = (2 * b - 1) * d;
+                        dir = vnormalize(refl + a * pr1 + b * pr2);
+                        loops++;
+                    } while (vdot(dir, h.normal) <= 0 && loops < P.glossy_ray_count / 4);
+                    if (vdot(dir, h.normal) > 0) {
+                        Ray g;
+                        g.origin = h.hitPoint + 0.01f * dir;
+                        g.direction = dir;
+                        mirror += final_color(sc, P, g, level + 1, cnt) * fmax_g(std::pow(vdot(refl, dir), s), 0.0f);
+                    }
+                }
                 color += m.ks * mirror / (float)P.glossy_ray_count;
             } else {
                 color += m.ks * mirror;
@@ -606,7 +666,15 @@ static Ray camera_ray(const Cam& c, float px, float py) {
     return r;
 }
 
+// one camera sample of the pixel (restarts the pixel's glossy draw stream for that sample)
+static V3 sample_color(Scene& sc, const rt_params& P, const Ray& r, int sample, Counter& cnt) {
+    cnt.sample = (uint32_t)sample;
+    cnt.draws = 0;
+    return final_color(sc, P, r, 0, cnt);
+}
+
 static V3 render_pixel(Scene& sc, const Cam& cam, const rt_params& P, int W, int H, int x, int y, Counter& cnt) {
+    cnt.pix = (uint32_t)(y * W + x);
     const float nx = float(x) / W * 2.0f - 1.0f;
     const float ny = float(y) / H * 2.0f - 1.0f;
     if (P.anti_aliasing) {
@@ -614,7 +682,7 @@ static V3 render_pixel(Scene& sc, const Cam& cam, const rt_params& P, int W, int
         const float qx[4] = {nx - ox, nx + ox, nx - ox, nx + ox};
         const float qy[4] = {ny + oy, ny + oy, ny - oy, ny - oy};
         V3 avg(0.0f);
-        for (int i = 0; i < 4; i++) avg += final_color(sc, P, camera_ray(cam, qx[i], qy[i]), 0, cnt);
+        for (int i = 0; i < 4; i++) avg += sample_color(sc, P, camera_ray(cam, qx[i], qy[i]), i, cnt);
         avg = avg * (float)0.25;
         return avg;
     }
@@ -624,14 +692,15 @@ static V3 render_pixel(Scene& sc, const Cam& cam, const rt_params& P, int W, int
         const int moves = std::sqrt(P.sample_size) - 1;
         const float sgn[4][2] = {{-1.0f, 1.0f}, {1.0f, 1.0f}, {-1.0f, -1.0f}, {1.0f, -1.0f}};
         V3 avg(0.0f);
+        int k = 0;
         for (int i = 0; i < 4; i++)
             for (int a = 1; a <= moves; a += 2)
                 for (int b = 1; b <= moves; b += 2)
-                    avg += final_color(
-                        sc, P, camera_ray(cam, nx + (ox * sgn[i][0] * a), ny + (oy * sgn[i][1] * b)), 0, cnt);
+                    avg += sample_color(
+                        sc, P, camera_ray(cam, nx + (ox * sgn[i][0] * a), ny + (oy * sgn[i][1] * b)), k++, cnt);
         return avg * (float)(1.0f / P.sample_size);
     }
-    return final_color(sc, P, camera_ray(cam, nx, ny), 0, cnt);
+    return sample_color(sc, P, camera_ray(cam, nx, ny), 0, cnt);
 }
 
 }  // namespace oracle
@@ -747,6 +816,7 @@ int oracle_shade(oracle_scene* o, const rt_ray* rays, int n, const rt_params* P,
         r.direction = V3::of(rays[i].direction);
         r.t = rays[i].t;
         Counter cnt;
+        cnt.pix = (uint32_t)i;
         const V3 c = final_color(o->sc, *P, r, 0, cnt);
         rgb[i * 3] = c.x;
         rgb[i * 3 + 1] = c.y;
@@ -798,6 +868,13 @@ int oracle_render(oracle_scene* o, const float look[3], const float euler[3], fl
         }
     }
     if (total_rays) *total_rays = total;
+    return 0;
+}
+
+int oracle_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+    uint32_t c[4] = {ctr[0], ctr[1], ctr[2], ctr[3]};
+    philox(c, (uint64_t)key[0] | ((uint64_t)key[1] << 32));
+    std::memcpy(out, c, sizeof(c));
     return 0;
 }
 

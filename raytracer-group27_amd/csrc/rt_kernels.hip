@@ -29,6 +29,7 @@ struct DMat {
     float ks[3];
     float shin;
     float transp;
+    float gd;  // glossy lobe half-width d = pow(0.5f, -1/s) * sqrt(1 - pow(0.5, 2/s)) (src/main.cpp:224), host-evaluated
 };
 struct DSph {
     float c[3];
@@ -36,7 +37,7 @@ struct DSph {
     DMat m;
     int key_bvh;
     int leaf;
-    int pad_[2];
+    int pad_[1];
 };
 struct DRefNode {
     float lo[3];
@@ -93,7 +94,30 @@ struct KParams {
     int leaf_batch;             // dynamic-fetch kernel: lanes with postponed leaves that start a leaf phase
     const float* pre_t;         // precomputed primary hits per job (rt_packet.hip), or null
     const int* pre_rec;
+    uint32_t seed_lo, seed_hi;  // glossy sampling: Philox-4x32-10 key (rt_params.rng_seed)
 };
+
+// Philox-4x32-10 (Salmon et al., SC'11; the Random123 constants): the counter-based stream that
+// replaces the reference's rand() for glossy lobes.  Counter = (draw, pixel, sample, 0).
+__host__ __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+    for (int r = 0; r < 10; ++r) {
+        if (r > 0) {
+            k0 += 0x9E3779B9u;
+            k1 += 0xBB67AE85u;
+        }
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
+        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+        c[1] = (uint32_t)p1;
+        c[3] = (uint32_t)p0;
+        c[0] = n0;
+        c[2] = n2;
+    }
+}
+
+// uniform float in [0, 1) from the top 24 bits (stands in for the reference's rand() / (float)RAND_MAX)
+__host__ __device__ __forceinline__ float u01(uint32_t x) { return (float)(x >> 8) * 5.9604644775390625e-8f; }
 
 struct Cnt {
     uint32_t rays, nodes, tris, hits;
@@ -573,13 +597,17 @@ __device__ v3 direct_light(const KParams& P, const Surf& s, v3 refl, int* stk, C
 //   mirror:      color += (ks * (0 + ks * child)) / glossy_ray_count   (or ks * (...) if shininess == 0)
 //   transparent: color += R * reflectChild;  color += (1-R) * refractChild   (src/main.cpp:191-290)
 // ------------------------------------------------------------------------------------------
-enum { FR_MIRROR = 0, FR_TRANS_A = 1, FR_TRANS_B = 2 };
+enum { FR_MIRROR = 0, FR_TRANS_A = 1, FR_TRANS_B = 2, FR_GLOSSY = 3 };
 struct Frame {
     v3 color;
-    v3 w;      // ks (mirror) | (reflectionChance, refractionChance, -) (transparent)
-    v3 o2, d2; // pending refracted ray
+    v3 w;      // ks (mirror, glossy) | (reflectionChance, refractionChance, -) (transparent)
+    v3 o2, d2; // pending refracted ray | glossy: reflectColor accumulator, reflect
     int mode;
-    int flag;  // mirror: shininess != 0 ; transparent: refracted ray traced
+    int flag;  // mirror: shininess != 0 ; transparent: refracted ray traced ; glossy: sample index
+    // glossy lobe (src/main.cpp:204-250): hit point, hitInfo.normal (unnormalised), current sample
+    // direction, shininess and the lobe half-width d (host-evaluated per material)
+    v3 hp, nraw, sdir;
+    float shin, gd;
 };
 
 template <bool COUNT>

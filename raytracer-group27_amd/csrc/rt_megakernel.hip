@@ -43,6 +43,9 @@ struct Lane {
     // cansee
     v3 so, sd;
     float sdist, sI;
+    // glossy lobes: hitInfo.normal of the shading point, Philox draw counter and pixel id
+    v3 nraw;
+    uint32_t draws, rpix;
 };
 
 __device__ __forceinline__ DMat load_mat(const DevScene& S, int m) {
@@ -549,6 +552,51 @@ __device__ bool advance_lights(const KParams& P, Lane& L, bool have_result, bool
     }
 }
 
+// ---- glossy lobe ---------------------------------------------------------------------------
+// Next lobe sample of the glossy frame f (src/main.cpp:209-249): two uniforms per draw from the
+// Philox stream (key = rng_seed, counter = (draw, pixel, sample, 0)) in place of rand(); up to
+// glossy_ray_count / 4 redraws while the direction points into the surface.  Returns true with
+// the sample ray queued; false when the lobe is done.
+__device__ bool glossy_next(const KParams& P, Lane& L, Frame& f) {
+    const v3 r = f.d2;
+    v3 notr = r;
+    if (r.x != 0.0f) {
+        notr.y = -r.x;
+        notr.x = r.y;
+    } else {
+        notr.y = -r.z;
+        notr.z = r.y;
+    }
+    const v3 pr1 = cross(r, notr);
+    const v3 pr2 = cross(r, pr1);
+    while (++f.flag < P.glossy_n) {
+        v3 sd;
+        int loops = 0;
+        do {
+            float a, b;
+            do {
+                uint32_t c[4] = {L.draws++, L.rpix, (uint32_t)L.sample, 0u};
+                philox4x32_10(c, P.seed_lo, P.seed_hi);
+                a = u01(c[0]);
+                b = u01(c[1]);
+            } while (a == 0.0f && b == 0.0f && a * a + b * b < 1.0f);
+            a = (2.0f * a - 1.0f) * f.gd;
+            b = (2.0f * b - 1.0f) * f.gd;
+            sd = normalize((r + a * pr1) + b * pr2);
+            loops++;
+        } while (dot(sd, f.nraw) <= 0.0f && loops < P.glossy_n / 4);
+        if (dot(sd, f.nraw) > 0.0f) {
+            f.sdir = sd;
+            L.qo = f.hp + 0.01f * sd;
+            L.qd = sd;
+            L.qt = FLT_MAX;
+            L.qtype = Q_PATH;
+            return true;
+        }
+    }
+    return false;
+}
+
 // ---- recursion tree ------------------------------------------------------------------------
 // After the direct light of the shading point at L.level: descend (returns true with the
 // child ray queued) or fold the finished subtree into its ancestors.  Returns false when the
@@ -565,6 +613,15 @@ __device__ bool finish_node(const KParams& P, Lane& L, Frame* fr, bool hit, v3& 
                 f.w = v3{m.ks[0], m.ks[1], m.ks[2]};
                 f.mode = FR_MIRROR;
                 f.flag = (m.shin != 0.0f);
+                if (f.flag && P.glossy_n > 1) {  // lobe samples follow the mirror ray
+                    f.mode = FR_GLOSSY;
+                    f.flag = 0;
+                    f.d2 = L.refl;
+                    f.hp = L.hp;
+                    f.nraw = L.nraw;
+                    f.shin = m.shin;
+                    f.gd = m.gd;
+                }
                 L.qo = L.hp + 0.01f * L.refl;
                 L.qd = L.refl;
                 L.qt = FLT_MAX;
@@ -604,6 +661,20 @@ __device__ bool finish_node(const KParams& P, Lane& L, Frame* fr, bool hit, v3& 
             const v3 rc = v3{0.0f, 0.0f, 0.0f} + f.w * child;
             const v3 add = f.flag ? (f.w * rc) / (float)P.glossy_n : f.w * rc;
             child = f.color + add;
+        } else if (f.mode == FR_GLOSSY) {
+            // reflectColor = 0 + ks * mirror child, then + child * max(pow(dot(reflect, dir), s), 0)
+            // per lobe sample that left the surface (src/main.cpp:197-250)
+            if (f.flag == 0) {
+                f.o2 = v3{0.0f, 0.0f, 0.0f} + f.w * child;
+            } else {
+                const float cw = powf(dot(f.d2, f.sdir), f.shin);
+                f.o2 = f.o2 + child * gmax(cw, 0.0f);
+            }
+            if (glossy_next(P, L, f)) {
+                L.level++;
+                return true;
+            }
+            child = f.color + (f.w * f.o2) / (float)P.glossy_n;
         } else if (f.mode == FR_TRANS_A) {
             f.color = f.color + f.w.x * child;
             if (f.flag) {
@@ -662,6 +733,8 @@ __device__ __forceinline__ void queue_camera(const KParams& P, Lane& L) {
     L.qt = FLT_MAX;
     L.qtype = Q_PATH;
     L.level = 0;
+    L.draws = 0u;
+    L.rpix = (uint32_t)(L.py * P.W + L.px);  // the reference's pixel (x, y), y up
 }
 
 // Map a job index to its pixel (8x8 tiles inside the rank's bands).  False if outside the image.
@@ -739,6 +812,8 @@ __global__ __launch_bounds__(64, WPE) void persistent_kernel(KParams P, JobSrc J
                         L.qt = r.t;
                         L.qtype = Q_PATH;
                         L.level = 0;
+                        L.draws = 0u;
+                        L.rpix = (uint32_t)job;
                         need_trace = true;
                     }
                 } else {
@@ -823,6 +898,7 @@ __global__ __launch_bounds__(64, WPE) void persistent_kernel(KParams P, JobSrc J
                 if (COUNT) cnt.hits++;
                 const Surf s = surface(S, L.qo, L.qd, b);
                 L.hp = s.p;
+                L.nraw = s.n;
                 L.nN = normalize(s.n);
                 L.refl = reflect(normalize(L.qd), L.nN);
                 L.nR = normalize(L.refl);
@@ -1119,6 +1195,7 @@ __device__ bool advance_lane(const KParams& P, const JobSrc& J, Lane& L, Frame* 
             if (COUNT) cnt.hits++;
             const Surf s = surface(S, L.qo, L.qd, b);
             L.hp = s.p;
+            L.nraw = s.n;
             L.nN = normalize(s.n);
             L.refl = reflect(normalize(L.qd), L.nN);
             L.nR = normalize(L.refl);
@@ -1226,6 +1303,8 @@ __global__ __launch_bounds__(64, WPE) void persistent_df_kernel(KParams P, JobSr
                         L.qt = r.t;
                         L.qtype = Q_PATH;
                         L.level = 0;
+                        L.draws = 0u;
+                        L.rpix = (uint32_t)job;
                         start = true;
                     }
                 } else {

@@ -215,6 +215,13 @@ extern "C" int rt_destroy(rt_ctx* c) {
     return RT_OK;
 }
 
+// glossy lobe half-width of getFinalColor (src/main.cpp:224), evaluated on the host with the
+// reference's float/double mix so every device (and the oracle) uses the same bits
+static float glossy_width(float shininess) {
+    if (shininess == 0.0f) return 0.0f;
+    return (float)((double)std::pow(0.5f, -1 / shininess) * std::sqrt(1 - std::pow(0.5, (double)(2 / shininess))));
+}
+
 extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
     if (!desc || !out) {
         set_error("rt_create: null argument");
@@ -354,6 +361,7 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
         }
         mats[m].shin = sm.shininess;
         mats[m].transp = sm.transparency;
+        mats[m].gd = glossy_width(sm.shininess);
         if (sm.transparency != 1.0f) all_opaque = false;
         if (sm.transparency == 1.0f && (sm.ks[0] > 0 || sm.ks[1] > 0 || sm.ks[2] > 0) && sm.shininess != 0.0f)
             c->glossy_material = true;
@@ -369,6 +377,7 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
         sph[s].r = ss.radius;
         sph[s].m.shin = ss.material.shininess;
         sph[s].m.transp = ss.material.transparency;
+        sph[s].m.gd = glossy_width(ss.material.shininess);
         sph[s].key_bvh = ref.sph_key[s];
         sph[s].leaf = ref.sph_leaf[s];
         if (ss.material.transparency != 1.0f) all_opaque = false;
@@ -450,8 +459,12 @@ static int fill_params(rt_ctx* c, const rt_camera* cam, const rt_params* p, int 
         set_error("max_reflection_level must be in [0, 15]");
         return RT_ERR_INVALID;
     }
-    if (p->glossy_ray_count != 1 && c->glossy_material && p->max_reflection_level > 0) {
-        set_error("glossy_ray_count > 1 with a glossy material is not supported yet (the reference uses rand())");
+    if (p->glossy_ray_count < 1) {
+        set_error("glossy_ray_count must be >= 1");
+        return RT_ERR_INVALID;
+    }
+    if (p->glossy_ray_count != 1 && c->glossy_material && p->max_reflection_level > 0 && use_tile_kernel()) {
+        set_error("glossy_ray_count > 1: the tile kernel has no glossy lobes (use the persistent kernels)");
         return RT_ERR_INVALID;
     }
     if (p->multiple_rays && !(p->sample_size == 4 || p->sample_size == 16 || p->sample_size == 64)) {
@@ -462,6 +475,8 @@ static int fill_params(rt_ctx* c, const rt_camera* cam, const rt_params* p, int 
     K.S = c->S;
     K.max_level = p->max_reflection_level;
     K.glossy_n = p->glossy_ray_count;
+    K.seed_lo = (uint32_t)(p->rng_seed & 0xFFFFFFFFull);
+    K.seed_hi = (uint32_t)(p->rng_seed >> 32);
     K.plane_k = p->plane_light_1D_ray_count;
     K.use_bvh = p->use_bvh ? 1 : 0;
     K.refr = p->refraction_factor;
@@ -963,6 +978,17 @@ extern "C" int rt_ctx_info(rt_ctx* c, int* num_nodes, int* num_tri_records, int*
     if (num_tri_records) *num_tri_records = c->nrec;
     if (ref_bvh_nodes) *ref_bvh_nodes = c->ref_nodes;
     if (ref_bvh_levels) *ref_bvh_levels = c->ref_levels;
+    return RT_OK;
+}
+
+extern "C" int rt_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+    if (!ctr || !key || !out) {
+        set_error("rt_philox4x32_10: null argument");
+        return RT_ERR_INVALID;
+    }
+    uint32_t c[4] = {ctr[0], ctr[1], ctr[2], ctr[3]};
+    philox4x32_10(c, key[0], key[1]);
+    for (int k = 0; k < 4; ++k) out[k] = c[k];
     return RT_OK;
 }
 

@@ -47,6 +47,8 @@ enum WfField {
     WF_U1 = WF_U0 + 3,
     WF_SDIST = WF_U1 + 3,
     WF_SI,
+    WF_NRAW,  // 3
+    WF_DRAWS = WF_NRAW + 3,
     WF_NFIELDS
 };
 
@@ -117,6 +119,8 @@ __device__ __forceinline__ void wf_load(const WfSt& S, int i, Lane& L, uint32_t&
     L.u1 = S.v(WF_U1, i);
     L.sdist = S.f(WF_SDIST, i);
     L.sI = S.f(WF_SI, i);
+    L.nraw = S.v(WF_NRAW, i);
+    L.draws = (uint32_t)S.n(WF_DRAWS, i);
     L.so = L.qo;
     L.sd = L.qd;
 }
@@ -149,6 +153,8 @@ __device__ __forceinline__ void wf_store(const WfSt& S, int i, const Lane& L, ui
     S.sv(WF_U1, i, L.u1);
     S.sf(WF_SDIST, i, L.sdist);
     S.sf(WF_SI, i, L.sI);
+    S.sv(WF_NRAW, i, L.nraw);
+    S.sn(WF_DRAWS, i, (int)L.draws);
 }
 
 // Wave-aggregated append: one atomic per wave; every lane of the wave must call it.
@@ -187,6 +193,9 @@ __global__ __launch_bounds__(64) void wf_seed_kernel(KParams P, JobSrc J, WfBufs
         L.a0 = L.a1 = L.a2 = L.a3 = 0.0f;
         L.sdist = 0.0f;
         L.sI = 1.0f;
+        L.nraw = v3{0.0f, 0.0f, 1.0f};
+        L.draws = 0u;
+        L.rpix = (uint32_t)job;
         L.qt = FLT_MAX;
         L.qtype = Q_PATH;
         L.qo = L.qd = v3{0.0f, 0.0f, 0.0f};
@@ -344,8 +353,10 @@ __global__ __launch_bounds__(64) void wf_shade_kernel(KParams P, JobSrc J, WfBuf
                 if (J.mode == 0) {
                     job_pixel(P, L.job, L);
                     L.nsamples = P.aa ? 4 : (P.multi ? P.sample_size : 1);
+                    L.rpix = (uint32_t)(L.py * P.W + L.px);
                 } else {
                     L.nsamples = 1;
+                    L.rpix = (uint32_t)L.job;
                 }
                 Best b;
                 b.t = W.res_t[qbase + i];
