@@ -212,6 +212,11 @@ int rt_shade(rt_ctx* ctx, const rt_ray* rays, int n, const rt_params* params, fl
 int rt_set_counting(int on);
 /* Debug counters of the last counting launch (per-query node-visit histogram, maxima). */
 int rt_debug_counters(rt_ctx* ctx, uint64_t* out, int n);
+/* Developer wave trace of the last persistent-kernel launch made with RT_WAVE_TRACE=1: 8 words
+ * per wave (start, end, jobs taken, time the job queue ran dry for it, drain iterations, sum of
+ * tracing lanes over them, 0, drain state-machine passes); timestamps of
+ * the 100 MHz device clock.  Out holds 8 * max_waves words.  Returns the wave count. */
+int rt_debug_wave_trace(rt_ctx* ctx, uint64_t* out, int max_waves);
 
 /* Introspection for tests / roofline accounting. */
 int rt_ctx_info(rt_ctx* ctx, int* num_nodes, int* num_tri_records, int* ref_bvh_nodes,

@@ -95,6 +95,12 @@ struct KParams {
     const float* pre_t;         // precomputed primary hits per job (rt_packet.hip), or null
     const int* pre_rec;
     uint32_t seed_lo, seed_hi;  // glossy sampling: Philox-4x32-10 key (rt_params.rng_seed)
+    unsigned long long* wave_trace;  // developer trace (RT_WAVE_TRACE=1): per wave (start, end, jobs), or null
+    const int* job_order;            // persistent kernels: k-th job handed out is job_order[k] (rt_schedule.hip), or null
+    int* job_cost;                   // persistent kernels (pixels): queries each job took, or null
+    int coop;                        // dynamic-fetch kernel: lane-group traversal of the drain's queries
+    int coop_max;                    // ... when at most this many queries are left in the wave
+    int coop_reserve;                // ... free pool slots kept for depth-first steps
 };
 
 // Philox-4x32-10 (Salmon et al., SC'11; the Random123 constants): the counter-based stream that
@@ -160,19 +166,24 @@ struct RefMask {
     uint32_t known, pass;
 };
 
-__device__ __forceinline__ bool leaf_reachable(const DevScene& S, int leaf, v3 o, v3 nd, RefMask& m) {
-    const int* p = S.leaf_path + leaf * 8;
+__device__ __forceinline__ bool leaf_reachable_p(const int* leaf_path, const DRefNode* refn, int leaf, v3 o, v3 nd,
+                                                 RefMask& m) {
+    const int* p = leaf_path + leaf * 8;
     const int cnt = p[0];
     for (int k = 1; k <= cnt; ++k) {
         const int node = p[k];
         const uint32_t bit = 1u << node;
         if (!(m.known & bit)) {
             m.known |= bit;
-            if (ref_slab(S.refn[node], o, nd)) m.pass |= bit;
+            if (ref_slab(refn[node], o, nd)) m.pass |= bit;
         }
         if (!(m.pass & bit)) return false;
     }
     return true;
+}
+
+__device__ __forceinline__ bool leaf_reachable(const DevScene& S, int leaf, v3 o, v3 nd, RefMask& m) {
+    return leaf_reachable_p(S.leaf_path, S.refn, leaf, o, nd, m);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -761,6 +761,8 @@ __global__ __launch_bounds__(64, WPE) void persistent_kernel(KParams P, JobSrc J
     __shared__ int s_base;
     const int lane_id = threadIdx.x;
     int* stk = stack_lds + lane_id;
+    const unsigned long long t_wave0 = P.wave_trace ? wall_clock64() : 0ull;
+    unsigned int wave_jobs = 0;  // jobs this wave took (wave trace)
     const DevScene& S = P.S;
     Frame fr[RT_MAX_DEPTH];
     Lane L;
@@ -776,13 +778,15 @@ __global__ __launch_bounds__(64, WPE) void persistent_kernel(KParams P, JobSrc J
         const unsigned long long want = __ballot(idle);
         if (want) {
             if (lane_id == __ffsll((long long)want) - 1) s_base = atomicAdd(J.counter, __popcll(want));
+            wave_jobs += (unsigned int)__popcll(want);
             __builtin_amdgcn_wave_barrier();
             __syncthreads();
             const int base = s_base;
             if (idle) {
                 const int myrank = __popcll(want & ((1ull << lane_id) - 1ull));
-                const int job = base + myrank;
-                if (job < J.njobs) {
+                const int job_k = base + myrank;
+                if (job_k < J.njobs) {
+                    const int job = P.job_order ? P.job_order[job_k] : job_k;  // longest-first order
                     L.job = job;
                     L.sample = 0;
                     L.pacc = v3{0.0f, 0.0f, 0.0f};
@@ -937,6 +941,7 @@ __global__ __launch_bounds__(64, WPE) void persistent_kernel(KParams P, JobSrc J
             dst[0] = col.x;
             dst[1] = col.y;
             dst[2] = col.z;
+            if (P.job_cost) P.job_cost[L.job] = (int)job_cnt.rays;  // queries of this pixel (schedule)
         } else {
             J.rgb[L.job * 3 + 0] = out.x;
             J.rgb[L.job * 3 + 1] = out.y;
@@ -946,6 +951,13 @@ __global__ __launch_bounds__(64, WPE) void persistent_kernel(KParams P, JobSrc J
         L.job = -1;
     }
     flush_counters<COUNT>(P, cnt);
+    if (P.wave_trace && lane_id == 0) {  // RT_WAVE_TRACE: (start, end, jobs) per wave, 100 MHz clock
+        unsigned long long* w = P.wave_trace + 8 * blockIdx.x;
+        w[0] = t_wave0;
+        w[1] = wall_clock64();
+        w[2] = wave_jobs;
+        for (int k = 3; k < 8; ++k) w[k] = 0ull;
+    }
 }
 
 
@@ -1129,6 +1141,281 @@ __device__ __forceinline__ void trav_record(const DevScene& S, Trav& T, Cnt& cnt
     }
 }
 
+// ---- cooperative drain traversal -----------------------------------------------------------
+// Once the job queue is dry a wave keeps few lanes with a query (tools/wave_trace.py: median 8
+// of 64 after the queue runs dry) and each of those walks its query one node or record per
+// dependent step: the frame ends with the longest such chain.  coop_group_trace gives each
+// remaining query (k <= COOP_Q of them) a group of G = 64/k lanes (power of two) that walks it
+// breadth first: each group lane visits one node of the group's pool per step and tests the
+// records of that node's hit leaves, so a step covers up to G nodes.  Candidates are judged with
+// the owner's arithmetic (tri_test, leaf_reachable) against the group's running best; the best
+// is the lexicographic minimum of (t, key) and an any-hit query takes any accepted candidate, so
+// every owner ends with the hit its own walk would give (tests/test_gpu_parity.py, RT_COOP=0 vs 1).
+#define COOP_POOL 2048  // node groups, split between the lane groups
+#define COOP_Q 16       // queries one drain traversal takes
+
+// query hand-over through LDS: [field][COOP_Q]
+enum {
+    CQ_OX, CQ_OY, CQ_OZ, CQ_DX, CQ_DY, CQ_DZ, CQ_NX, CQ_NY, CQ_NZ, CQ_IX, CQ_IY, CQ_IZ,
+    CQ_THR, CQ_TCULL, CQ_BT, CQ_BKEY, CQ_BREC, CQ_FLAGS, CQ_MK, CQ_MP, CQ_TOP, CQ_RR, CQ_RK, CQ_LB, CQ_LC, CQ_LH,
+    CQ_N
+};
+
+__device__ __forceinline__ void coop_put(const Trav& T, int* q, int r) {
+    const float f[12] = {T.o.x, T.o.y, T.o.z, T.d.x, T.d.y, T.d.z, T.nd.x, T.nd.y, T.nd.z, T.inv.x, T.inv.y, T.inv.z};
+#pragma unroll
+    for (int i = 0; i < 12; ++i) q[i * COOP_Q + r] = __float_as_int(f[i]);
+    q[CQ_THR * COOP_Q + r] = __float_as_int(T.thr);
+    q[CQ_TCULL * COOP_Q + r] = __float_as_int(T.tcull);
+    q[CQ_BT * COOP_Q + r] = __float_as_int(T.best.t);
+    q[CQ_BKEY * COOP_Q + r] = T.best.key;
+    q[CQ_BREC * COOP_Q + r] = T.best.rec;
+    q[CQ_FLAGS * COOP_Q + r] = (T.found ? 1 : 0) | (T.ref ? 2 : 0) | (T.any ? 4 : 0);
+    q[CQ_MK * COOP_Q + r] = (int)T.mask.known;
+    q[CQ_MP * COOP_Q + r] = (int)T.mask.pass;
+    q[CQ_TOP * COOP_Q + r] = T.sp + (T.cur != RT_TRAV_NONE ? 1 : 0);
+    q[CQ_RR * COOP_Q + r] = T.rr;
+    q[CQ_RK * COOP_Q + r] = T.rk;
+    q[CQ_LB * COOP_Q + r] = (int)T.lb;
+    q[CQ_LC * COOP_Q + r] = (int)T.lc;
+    q[CQ_LH * COOP_Q + r] = (int)T.lh;
+}
+
+// the owner's query after coop_group_trace: its hit, nothing left to walk
+__device__ __forceinline__ void coop_get(Trav& T, const int* q, int r) {
+    T.best.t = __int_as_float(q[CQ_BT * COOP_Q + r]);
+    T.best.key = q[CQ_BKEY * COOP_Q + r];
+    T.best.rec = q[CQ_BREC * COOP_Q + r];
+    T.found = (q[CQ_FLAGS * COOP_Q + r] & 1) != 0;
+    T.tcull = __int_as_float(q[CQ_TCULL * COOP_Q + r]);
+    T.mask.known = (uint32_t)q[CQ_MK * COOP_Q + r];
+    T.mask.pass = (uint32_t)q[CQ_MP * COOP_Q + r];
+    T.cur = RT_TRAV_NONE;
+    T.sp = 0;
+    T.rk = 0;
+    T.lh = 0u;
+}
+
+__device__ __forceinline__ void lex_min(float& t, int& key, int& rec, float t2, int key2, int rec2) {
+    if (t2 < t || (t2 == t && key2 < key)) {
+        t = t2;
+        key = key2;
+        rec = rec2;
+    }
+}
+
+// Box tests of the slots `slots` of one quantised BVH8 node (the arithmetic of trav_node): hit
+// masks of inner and leaf children against the cull distance tc, the node's child base, record
+// base and 4-bit record counts.
+template <int NW>
+__device__ __forceinline__ void node_slot_hits(const float4* np, v3 o, v3 inv, float tc, uint32_t slots, uint32_t& ih,
+                                               uint32_t& lh, uint32_t& child_base, uint32_t& tri_base,
+                                               uint32_t& counts, uint32_t& imask_out) {
+    const float4 f0 = np[0], f1 = np[1], qlx = np[2], qly = np[3], qlz = np[4], qhx = np[5], qhy = np[6],
+                 qhz = np[7];
+    const uint32_t w3 = __float_as_uint(f0.w);
+    const uint32_t imask = __float_as_uint(f1.z) & 0xFFu;
+    const uint32_t lmask = (__float_as_uint(f1.z) >> 8) & 0xFFu;
+    child_base = __float_as_uint(f1.x);
+    tri_base = __float_as_uint(f1.y);
+    counts = __float_as_uint(f1.w);
+    imask_out = imask;
+    const float bx = pow2f(w3 & 0xFFu) * inv.x, by = pow2f((w3 >> 8) & 0xFFu) * inv.y,
+                bz = pow2f((w3 >> 16) & 0xFFu) * inv.z;
+    const float ax = (f0.x - o.x) * inv.x, ay = (f0.y - o.y) * inv.y, az = (f0.z - o.z) * inv.z;
+    const uint32_t m = slots & (imask | lmask);
+    uint32_t hits = 0;
+#pragma unroll
+    for (int s = 0; s < NW; ++s) {
+        if (m & (1u << s)) {
+            const int wi = s >> 1, sh = (s & 1) * 16;
+            auto q = [&](const float4& f) {
+                const uint32_t wv = __float_as_uint(wi == 0 ? f.x : wi == 1 ? f.y : wi == 2 ? f.z : f.w);
+                return (float)((wv >> sh) & 0xFFFFu);
+            };
+            const float tlx = fmaf(q(qlx), bx, ax), thx = fmaf(q(qhx), bx, ax);
+            const float tly = fmaf(q(qly), by, ay), thy = fmaf(q(qhy), by, ay);
+            const float tlz = fmaf(q(qlz), bz, az), thz = fmaf(q(qhz), bz, az);
+            const float t0 = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fminf(tlz, thz));
+            const float t1 = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fmaxf(tlz, thz));
+            if (t0 <= t1 && t1 >= 0.0f && t0 <= tc) hits |= 1u << s;
+        }
+    }
+    ih = hits & imask;
+    lh = hits & lmask;
+}
+
+// exclusive prefix of v over the aligned group of G lanes; group total in `tot`
+__device__ __forceinline__ int group_scan(int v, int G, int gl, int& tot) {
+    int inc = v;
+    for (int off = 1; off < G; off <<= 1) {
+        const int u = __shfl_up(inc, off, G);
+        if (gl >= off) inc += u;
+    }
+    tot = __shfl(inc, G - 1, G);
+    return inc - v;
+}
+
+// The drain traversal.  `om`: lanes that own a query; the r-th owner's query is q[.][r] and its
+// node groups (LDS stack, then the node it was about to visit) are pool[r * PC ..].  Results go
+// back into q[.][r].
+// Returns this lane's (node visits, record tests).
+template <int NW>
+__device__ __forceinline__ uint2 coop_group_trace(const float4* __restrict__ nodes, const float4* __restrict__ tri,
+                                               const DRefNode* __restrict__ refn, const int* __restrict__ leaf_path,
+                                               int* pool, int* q, unsigned long long om, int reserve) {
+    const int lane = (int)(threadIdx.x & 63);
+    const int k = __popcll(om);
+    int G = 64;
+    while (G > 1 && k * G > 64) G >>= 1;
+    const int gi = lane / G, gl = lane % G;
+    const bool in_group = gi < k;
+    const int qi = in_group ? gi : 0;
+    const int PC = COOP_POOL * G / 64;
+    int* gpool = pool + qi * PC;
+    const v3 o{__int_as_float(q[CQ_OX * COOP_Q + qi]), __int_as_float(q[CQ_OY * COOP_Q + qi]),
+               __int_as_float(q[CQ_OZ * COOP_Q + qi])};
+    const v3 d{__int_as_float(q[CQ_DX * COOP_Q + qi]), __int_as_float(q[CQ_DY * COOP_Q + qi]),
+               __int_as_float(q[CQ_DZ * COOP_Q + qi])};
+    const v3 nd{__int_as_float(q[CQ_NX * COOP_Q + qi]), __int_as_float(q[CQ_NY * COOP_Q + qi]),
+                __int_as_float(q[CQ_NZ * COOP_Q + qi])};
+    const v3 inv{__int_as_float(q[CQ_IX * COOP_Q + qi]), __int_as_float(q[CQ_IY * COOP_Q + qi]),
+                 __int_as_float(q[CQ_IZ * COOP_Q + qi])};
+    const float thr = __int_as_float(q[CQ_THR * COOP_Q + qi]);
+    float tcull = __int_as_float(q[CQ_TCULL * COOP_Q + qi]);
+    float bt = __int_as_float(q[CQ_BT * COOP_Q + qi]);
+    int bkey = q[CQ_BKEY * COOP_Q + qi];
+    int brec = q[CQ_BREC * COOP_Q + qi];
+    const int flags = q[CQ_FLAGS * COOP_Q + qi];
+    bool found = (flags & 1) != 0;
+    const bool ref = (flags & 2) != 0, any = (flags & 4) != 0;
+    RefMask rm{(uint32_t)q[CQ_MK * COOP_Q + qi], (uint32_t)q[CQ_MP * COOP_Q + qi]};
+    int top = q[CQ_TOP * COOP_Q + qi];
+    // the owner's postponed leaf work goes to the group's first lane
+    int rr = 0, rk = 0;
+    uint32_t lb = 0u, lc = 0u, lh = 0u;
+    if (gl == 0) {
+        rr = q[CQ_RR * COOP_Q + qi];
+        rk = q[CQ_RK * COOP_Q + qi];
+        lb = (uint32_t)q[CQ_LB * COOP_Q + qi];
+        lc = (uint32_t)q[CQ_LC * COOP_Q + qi];
+        lh = (uint32_t)q[CQ_LH * COOP_Q + qi];
+    }
+    uint2 n{0u, 0u};
+    bool done = !in_group || (any && found);
+    for (;;) {
+        // ---- this lane's leaf records, against the group's best at the start of the step ----
+        float ct = FLT_MAX;
+        int ckey = 0x7fffffff, crec = RT_NO_HIT;
+        int acc_any = 0;
+        if (!done) {
+            float lt = bt;
+            int lkey = bkey;
+            for (;;) {
+                if (rk == 0) {
+                    if (!lh) break;
+                    const int s = __ffs(lh) - 1;
+                    lh &= lh - 1u;
+                    const uint32_t below = s ? (lc & ((1u << (4 * s)) - 1u)) : 0u;
+                    uint32_t nib = (below & 0x0F0F0F0Fu) + ((below >> 4) & 0x0F0F0F0Fu);
+                    nib = (nib * 0x01010101u) >> 24;
+                    rr = (int)(lb + nib);
+                    rk = (int)((lc >> (4 * s)) & 15u);
+                    continue;
+                }
+                const int r = rr++;
+                --rk;
+                const float4* tp = tri + (size_t)r * 4;
+                const float4 r0 = tp[0], r1 = tp[1], r2 = tp[2], r3 = tp[3];
+                n.y++;
+                float t;
+                if (!tri_test(r0, r1, r2, r3, o, d, nd, t)) continue;
+                const int key = ref ? __float_as_int(r3.z) : __float_as_int(r3.y);
+                bool acc = any ? (t <= thr) : (t < lt || (t == lt && key < lkey));
+                if (acc && ref && !leaf_reachable_p(leaf_path, refn, __float_as_int(r3.w), o, nd, rm)) acc = false;
+                if (!acc) continue;
+                lt = t;
+                lkey = key;
+                ct = t;
+                ckey = key;
+                crec = r;
+                acc_any = 1;
+                if (any) {
+                    rk = 0;
+                    lh = 0u;
+                    break;
+                }
+            }
+        }
+        // ---- group reduction (aligned xor butterfly, stays inside the group) ----
+        for (int off = G >> 1; off > 0; off >>= 1) {
+            const float t2 = __shfl_xor(ct, off);
+            const int k2 = __shfl_xor(ckey, off), r2 = __shfl_xor(crec, off);
+            acc_any |= __shfl_xor(acc_any, off);
+            lex_min(ct, ckey, crec, t2, k2, r2);
+        }
+        if (!done && acc_any) {
+            if (any) {  // any accepted candidate ends the query
+                bt = ct;
+                bkey = ckey;
+                brec = crec;
+                found = true;
+                done = true;
+            } else if (ct < bt || (ct == bt && ckey < bkey)) {
+                bt = ct;
+                bkey = ckey;
+                brec = crec;
+                found = true;
+                tcull = bt;
+            }
+        }
+        if (!done && top == 0) done = true;
+        if (!__any(!done)) break;
+        // ---- nodes: each group lane visits one node of its group's pool ----
+        // breadth (up to G nodes) while `reserve` pool slots stay free, else one node per step
+        // from the pool top (depth first): a visit grows the pool by at most NW - 1, and depth
+        // first by at most (NW - 1) per BVH level, which the reserve covers
+        int take = 0;
+        if (!done) {
+            take = min(G, top);
+            take = max(1, min(take, (PC - reserve - top) / (NW - 1)));
+        }
+        const bool mine = !done && gl < take;
+        const uint32_t item = mine ? (uint32_t)gpool[top - 1 - gl] : 0u;
+        if (!done) top -= take;
+        __syncthreads();
+        uint32_t ih = 0u, cb = 0u, imask = 0u;
+        if (mine) {
+            n.x++;
+            node_slot_hits<NW>(nodes + (size_t)(item >> 8) * 8, o, inv, any ? thr : tcull, item & 0xFFu, ih, lh, cb,
+                               lb, lc, imask);
+            rk = 0;
+        }
+        int ti = 0;
+        const int pi = group_scan(__popc(ih), G, gl, ti);
+        if (!done) {
+            int w = top + pi;
+            for (uint32_t m = ih; m; m &= m - 1u) {
+                const int s = __ffs(m) - 1;
+                if (w < PC) gpool[w] = (int)(((cb + __popc(imask & ((1u << s) - 1u))) << 8) | 0xFFu);
+                ++w;
+            }
+            top = min(PC, top + ti);
+        }
+        __syncthreads();
+    }
+    if (in_group && gl == 0) {
+        q[CQ_BT * COOP_Q + gi] = __float_as_int(bt);
+        q[CQ_BKEY * COOP_Q + gi] = bkey;
+        q[CQ_BREC * COOP_Q + gi] = brec;
+        q[CQ_FLAGS * COOP_Q + gi] = (found ? 1 : 0) | (ref ? 2 : 0) | (any ? 4 : 0);
+        q[CQ_TCULL * COOP_Q + gi] = __float_as_int(tcull);
+        q[CQ_MK * COOP_Q + gi] = (int)rm.known;
+        q[CQ_MP * COOP_Q + gi] = (int)rm.pass;
+    }
+    return n;
+}
+
 // Epilogue of trace_query8: the spheres, after every triangle (same order and keys).
 __device__ __forceinline__ void trav_finish(const DevScene& S, Trav& T) {
     if (T.any && T.found) return;
@@ -1226,6 +1513,7 @@ __device__ bool advance_lane(const KParams& P, const JobSrc& J, Lane& L, Frame* 
         dst[0] = col.x;
         dst[1] = col.y;
         dst[2] = col.z;
+        if (P.job_cost) P.job_cost[L.job] = (int)job_cnt.rays;  // queries of this pixel (schedule)
     } else {
         J.rgb[L.job * 3 + 0] = out.x;
         J.rgb[L.job * 3 + 1] = out.y;
@@ -1238,10 +1526,14 @@ __device__ bool advance_lane(const KParams& P, const JobSrc& J, Lane& L, Frame* 
 
 template <bool COUNT, int WPE, int BW>
 __global__ __launch_bounds__(64, WPE) void persistent_df_kernel(KParams P, JobSrc J) {
-    __shared__ int stack_lds[RT_STACK_SIZE * RT_WAVE];
+    __shared__ int stack_lds[RT_STACK8 * RT_WAVE];
+    __shared__ int coop_pool[COOP_POOL];   // drain: node groups of the wave's last queries
+    __shared__ int coop_q[CQ_N * COOP_Q];  // drain: those queries
     __shared__ int s_base;
     const int lane_id = threadIdx.x;
     int* stk = stack_lds + lane_id;
+    const unsigned long long t_wave0 = P.wave_trace ? wall_clock64() : 0ull;
+    unsigned int wave_jobs = 0;  // jobs this wave took (wave trace)
     const DevScene& S = P.S;
     Frame fr[RT_MAX_DEPTH];
     Lane L;
@@ -1253,9 +1545,13 @@ __global__ __launch_bounds__(64, WPE) void persistent_df_kernel(KParams P, JobSr
     bool pending = false;          // a finished query waits for advance_lane
     const int refill_at = P.refill;
     const int leaf_batch = P.leaf_batch;
+    // wave trace of the drain (after this wave first found the job queue empty)
+    unsigned long long t_exh = 0ull;
+    unsigned int it_drain = 0, lanes_drain = 0, coop_n = 0, pa_drain = 0;
     for (;;) {
         // ---- phase A: advance the pending lanes, then refill the idle ones ----
         unsigned long long tA = COUNT ? (unsigned long long)clock64() : 0ull;
+        if (P.wave_trace && t_exh) pa_drain++;
         bool start = false;
         if (pending) {
             pending = false;
@@ -1266,12 +1562,14 @@ __global__ __launch_bounds__(64, WPE) void persistent_df_kernel(KParams P, JobSr
         const unsigned long long want = __ballot(idle);
         if (want) {
             if (lane_id == __ffsll((long long)want) - 1) s_base = atomicAdd(J.counter, __popcll(want));
+            wave_jobs += (unsigned int)__popcll(want);
             __builtin_amdgcn_wave_barrier();
             __syncthreads();
             const int base = s_base;
             if (idle) {
-                const int job = base + __popcll(want & ((1ull << lane_id) - 1ull));
-                if (job < J.njobs) {
+                const int job_k = base + __popcll(want & ((1ull << lane_id) - 1ull));
+                if (job_k < J.njobs) {
+                    const int job = P.job_order ? P.job_order[job_k] : job_k;  // longest-first order
                     L.job = job;
                     L.sample = 0;
                     L.pacc = v3{0.0f, 0.0f, 0.0f};
@@ -1319,6 +1617,7 @@ __global__ __launch_bounds__(64, WPE) void persistent_df_kernel(KParams P, JobSr
             trav_init(P, L, T);
             tracing = true;
         }
+        if (P.wave_trace && !t_exh && __any(L.job == -2)) t_exh = wall_clock64();
         if (!__any(tracing)) {
             if (!__any(L.job == -1 || pending)) break;  // every lane exhausted
             continue;
@@ -1349,6 +1648,36 @@ __global__ __launch_bounds__(64, WPE) void persistent_df_kernel(KParams P, JobSr
                 }
                 if (!__any(tracing)) break;
                 if (__popcll(__ballot(pending || L.job == -1)) >= refill_at) break;
+                if (P.wave_trace && t_exh) {
+                    it_drain++;
+                    lanes_drain += (unsigned int)__popcll(__ballot(tracing));
+                }
+                // drain (no lane can take a new job): the remaining queries go to lane groups
+                if (P.coop && !__any(L.job == -1) && __any(L.job == -2)) {
+                    const unsigned long long om = __ballot(tracing);
+                    const int k = __popcll(om);
+                    if (k <= P.coop_max) {
+                        int G = 64;
+                        while (G > 1 && k * G > 64) G >>= 1;
+                        const int r = __popcll(om & ((1ull << lane_id) - 1ull));
+                        if (tracing) {
+                            coop_put(T, coop_q, r);
+                            int* gp = coop_pool + r * (COOP_POOL * G / 64);
+                            for (int j = 0; j < T.sp; ++j) gp[j] = stk[j * RT_WAVE];
+                            if (T.cur != RT_TRAV_NONE) gp[T.sp] = (int)T.cur;
+                        }
+                        __syncthreads();
+                        const uint2 nv = coop_group_trace<BW>(S.nodes, S.tri, S.refn, S.leaf_path, coop_pool, coop_q,
+                                                              om, P.coop_reserve);
+                        __syncthreads();
+                        if (COUNT) {
+                            cnt.nodes += nv.x;
+                            cnt.tris += nv.y;
+                        }
+                        if (tracing) coop_get(T, coop_q, r);
+                        if (P.wave_trace) coop_n++;
+                    }
+                }
                 continue;
             }
             const bool visit = tracing && !leaf_pending(T) && T.cur != RT_TRAV_NONE;
@@ -1377,6 +1706,17 @@ __global__ __launch_bounds__(64, WPE) void persistent_df_kernel(KParams P, JobSr
         if (COUNT) cnt.cyc_b += (unsigned long long)clock64() - tB;
     }
     flush_counters<COUNT>(P, cnt);
+    if (P.wave_trace && lane_id == 0) {  // RT_WAVE_TRACE, 100 MHz clock: start, end, jobs, drain
+        unsigned long long* w = P.wave_trace + 8 * blockIdx.x;
+        w[0] = t_wave0;
+        w[1] = wall_clock64();
+        w[2] = wave_jobs;
+        w[3] = t_exh;
+        w[4] = it_drain;
+        w[5] = lanes_drain;
+        w[6] = coop_n;
+        w[7] = pa_drain;
+    }
 }
 
 }  // namespace rt

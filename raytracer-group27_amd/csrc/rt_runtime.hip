@@ -19,6 +19,7 @@
 #include "rt_megakernel.hip"
 #include "rt_wavefront.hip"
 #include "rt_packet.hip"
+#include "rt_schedule.hip"
 
 using namespace rt;
 
@@ -55,6 +56,18 @@ struct rt_ctx {
     float* d_pre = nullptr;  // pre_t[njobs] | pre_rec[njobs]
     size_t pre_bytes = 0;
     int bvh8_depth = 0;
+    bool df_ok = true;
+    // longest-first schedule (rt_schedule.hip): tile hits | tile offsets | job order
+    float* d_sched = nullptr;
+    size_t sched_bytes = 0;
+    // cost-ordered schedule (RT_SCHED=2): per-job query counts of the previous frame + partition
+    float* d_cost = nullptr;  // cost[njobs] | block hist [16][nblk] | order[njobs]
+    size_t cost_bytes = 0;
+    long long cost_key = -1;  // launch geometry the stored costs belong to
+    // developer wave trace (RT_WAVE_TRACE=1)
+    float* d_wave_trace = nullptr;
+    size_t wave_trace_bytes = 0;
+    int wave_trace_n = 0;
 };
 
 // waves per SIMD the persistent kernel is compiled for (register cap); RT_WPE overrides for A/B runs
@@ -100,8 +113,8 @@ static int leaf_batch_threshold() {
 }
 
 template <bool COUNT, int BW>
-static void launch_wide(int grid, hipStream_t st, const KParams& K, const JobSrc& J) {
-    if (!use_whole_traversal_kernel(K.S.ntri)) {
+static void launch_wide(int grid, hipStream_t st, const KParams& K, const JobSrc& J, bool df_ok) {
+    if (df_ok && !use_whole_traversal_kernel(K.S.ntri)) {
         if (wpe() == 1)
             hipLaunchKernelGGL((persistent_df_kernel<COUNT, 1, BW>), dim3(grid), dim3(64), 0, st, K, J);
         else if (wpe() == 4)
@@ -123,9 +136,9 @@ static void launch_persistent(int grid, hipStream_t st, KParams K, const JobSrc&
     if (c->bw > 2) {
         K.S = c->S8;
         if (c->bw == 4)
-            launch_wide<COUNT, 4>(grid, st, K, J);
+            launch_wide<COUNT, 4>(grid, st, K, J, c->df_ok);
         else
-            launch_wide<COUNT, 8>(grid, st, K, J);
+            launch_wide<COUNT, 8>(grid, st, K, J, c->df_ok);
     } else {
         if (wpe() == 1)
             hipLaunchKernelGGL((persistent_kernel<COUNT, 1, 2>), dim3(grid), dim3(64), 0, st, K, J);
@@ -208,6 +221,9 @@ extern "C" int rt_destroy(rt_ctx* c) {
     if (c->d_wf_frames) hipFree(c->d_wf_frames);
     if (c->d_wf_cnt) hipFree(c->d_wf_cnt);
     if (c->d_pre) hipFree(c->d_pre);
+    if (c->d_wave_trace) hipFree(c->d_wave_trace);
+    if (c->d_sched) hipFree(c->d_sched);
+    if (c->d_cost) hipFree(c->d_cost);
     if (c->h_wf_cnt) hipHostFree(c->h_wf_cnt);
     for (hipEvent_t e : c->wf_ev) hipEventDestroy(e);
     if (c->stream) hipStreamDestroy(c->stream);
@@ -332,6 +348,7 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
         return RT_ERR_INVALID;
     }
     c->bvh8_depth = bvh8.max_depth;
+    c->df_ok = bvh8.max_depth + 2 < RT_STACK8;  // the dynamic-fetch kernel's smaller LDS stack
     if (c->bw > 2 && (bvh8.max_depth + 2 >= RT_STACK_SIZE || (int)bvh8.order.size() != ntri)) {
         set_error("rt_create: BVH8 deeper than the traversal stack");
         delete c;
@@ -513,6 +530,21 @@ static int fill_params(rt_ctx* c, const rt_camera* cam, const rt_params* p, int 
     K.aa_offy = 1.0f / (float)H * 0.25f;
     K.stats = c->d_stats;
     K.refill = refill_threshold();
+    {
+        const char* cp = std::getenv("RT_COOP");  // drain-phase cooperative traversal (default on)
+        K.coop = (cp && cp[0] == '0') ? 0 : 1;
+        // a group of G lanes owns COOP_POOL * G / 64 pool slots: the depth-first reserve plus one
+        // breadth step must fit; coop_max = the largest query count whose groups still do
+        K.coop_reserve = 7 * (c->bvh8_depth + 1) + 8;
+        K.coop_max = 0;
+        for (int k = 1; k <= COOP_Q; ++k) {
+            int G = 64;
+            while (G > 1 && k * G > 64) G >>= 1;
+            if (COOP_POOL * G / 64 >= K.coop_reserve + 8 * G) K.coop_max = k;
+        }
+        if (const char* cm = std::getenv("RT_COOP_MAX")) K.coop_max = std::min(K.coop_max, std::atoi(cm));
+        if (K.coop_max <= 0) K.coop = 0;
+    }
     K.leaf_batch = leaf_batch_threshold();
     return RT_OK;
 }
@@ -742,6 +774,76 @@ static int launch_packets(rt_ctx* c, KParams& K, hipStream_t st, int count_mode,
     return RT_OK;
 }
 
+// Longest-first schedule: primary pass + hit-first job order (rt_schedule.hip).  RT_SCHED=0
+// disables it; it needs one camera ray per pixel and the wide BVH.
+static bool use_schedule(const rt_ctx* c, const KParams& K) {
+    const char* v = std::getenv("RT_SCHED");
+    if (!v || v[0] != '1') return false;  // opt-in: measured no gain
+    return c->bw > 2 && !K.aa && !K.multi;
+}
+
+static int launch_schedule(rt_ctx* c, KParams& K, hipStream_t st, int count_mode, int njobs) {
+    const int ntiles = (njobs + 63) / 64;
+    int rc = ensure(c, &c->d_pre, &c->pre_bytes, (size_t)2 * njobs * sizeof(float));
+    if (rc != RT_OK) return rc;
+    rc = ensure(c, &c->d_sched, &c->sched_bytes, ((size_t)2 * (ntiles + 1) + njobs) * sizeof(int));
+    if (rc != RT_OK) return rc;
+    float* pt = c->d_pre;
+    int* pr = reinterpret_cast<int*>(c->d_pre + njobs);
+    int* hits = reinterpret_cast<int*>(c->d_sched);
+    int* off = hits + (ntiles + 1);
+    int* order = off + (ntiles + 1);
+    KParams Kp = K;
+    Kp.S = c->S8;
+    int cus = 0;
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
+    const int grid = std::min(ntiles, std::max(1, cus) * 16);
+    if (c->bw == 4) {
+        if (count_mode)
+            hipLaunchKernelGGL((primary_kernel<true, 4>), dim3(grid), dim3(64), 0, st, Kp, pt, pr, hits, ntiles);
+        else
+            hipLaunchKernelGGL((primary_kernel<false, 4>), dim3(grid), dim3(64), 0, st, Kp, pt, pr, hits, ntiles);
+    } else {
+        if (count_mode)
+            hipLaunchKernelGGL((primary_kernel<true, 8>), dim3(grid), dim3(64), 0, st, Kp, pt, pr, hits, ntiles);
+        else
+            hipLaunchKernelGGL((primary_kernel<false, 8>), dim3(grid), dim3(64), 0, st, Kp, pt, pr, hits, ntiles);
+    }
+    hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, st, hits, off, ntiles);
+    hipLaunchKernelGGL(job_order_kernel, dim3(grid), dim3(64), 0, st, pr, off, order, Kp, ntiles);
+    HIP_TRY(hipGetLastError());
+    K.pre_t = pt;
+    K.pre_rec = pr;
+    K.job_order = order;
+    return RT_OK;
+}
+
+// RT_SCHED=2: jobs ordered by the previous frame's per-pixel query counts (most expensive first).
+static int launch_cost_schedule(rt_ctx* c, KParams& K, hipStream_t st, int njobs) {
+    const int nblk = (njobs + CS_BLOCK - 1) / CS_BLOCK;
+    const size_t bytes = ((size_t)2 * njobs + (size_t)CS_BUCKETS * nblk) * sizeof(int);
+    const long long key = ((long long)K.W * 65536 + K.H) * 4096 + (long long)K.band_rank * 64 + K.band_count +
+                          ((long long)K.band_rows << 40);
+    const bool fresh = (c->cost_bytes < bytes) || (c->cost_key != key);
+    int rc = ensure(c, &c->d_cost, &c->cost_bytes, bytes);
+    if (rc != RT_OK) return rc;
+    int* cost = reinterpret_cast<int*>(c->d_cost);
+    int* hist = cost + njobs;
+    int* order = hist + (size_t)CS_BUCKETS * nblk;
+    if (fresh) {
+        HIP_TRY(hipMemsetAsync(cost, 0, (size_t)njobs * sizeof(int), st));
+        c->cost_key = key;
+    } else {
+        hipLaunchKernelGGL(cost_hist_kernel, dim3(nblk), dim3(CS_BLOCK), 0, st, cost, njobs, hist);
+        hipLaunchKernelGGL(cost_scan_kernel, dim3(1), dim3(1024), 0, st, hist, CS_BUCKETS * nblk);
+        hipLaunchKernelGGL(cost_scatter_kernel, dim3(nblk), dim3(CS_BLOCK), 0, st, cost, njobs, hist, order);
+        HIP_TRY(hipGetLastError());
+        K.job_order = order;
+    }
+    K.job_cost = cost;
+    return RT_OK;
+}
+
 static int launch_render(rt_ctx* c, KParams& K, hipStream_t st, int count_mode, rt_stats* stats) {
     const int tiles_x = (K.W + 7) / 8;
     const int tiles_y = (K.band_rows + 7) / 8;
@@ -771,8 +873,23 @@ static int launch_render(rt_ctx* c, KParams& K, hipStream_t st, int count_mode, 
             if (use_packets(c, K)) {
                 const int rc = launch_packets(c, K, st, count_mode, J.njobs);
                 if (rc != RT_OK) return rc;
+            } else if (use_schedule(c, K)) {
+                const int rc = launch_schedule(c, K, st, count_mode, J.njobs);
+                if (rc != RT_OK) return rc;
+            }
+            const char* cs = std::getenv("RT_SCHED");
+            if (cs && cs[0] == '2' && !K.job_order) {
+                const int rc = launch_cost_schedule(c, K, st, J.njobs);
+                if (rc != RT_OK) return rc;
             }
             const int grid = (int)std::min<long long>(blocks, persistent_grid(c));
+            const char* wt = std::getenv("RT_WAVE_TRACE");
+            if (wt && wt[0] == '1') {
+                const int rc = ensure(c, &c->d_wave_trace, &c->wave_trace_bytes, (size_t)grid * 8 * 8);
+                if (rc != RT_OK) return rc;
+                K.wave_trace = reinterpret_cast<unsigned long long*>(c->d_wave_trace);
+                c->wave_trace_n = grid;
+            }
             if (count_mode)
                 launch_persistent<true>(grid, st, K, J, c);
             else
@@ -979,6 +1096,13 @@ extern "C" int rt_ctx_info(rt_ctx* c, int* num_nodes, int* num_tri_records, int*
     if (ref_bvh_nodes) *ref_bvh_nodes = c->ref_nodes;
     if (ref_bvh_levels) *ref_bvh_levels = c->ref_levels;
     return RT_OK;
+}
+
+extern "C" int rt_debug_wave_trace(rt_ctx* c, uint64_t* out, int max_waves) {
+    if (!c || !out || max_waves <= 0) return RT_ERR_INVALID;
+    const int n = std::min(max_waves, c->wave_trace_n);
+    if (n > 0) HIP_TRY(hipMemcpy(out, c->d_wave_trace, (size_t)n * 8 * 8, hipMemcpyDeviceToHost));
+    return n;
 }
 
 extern "C" int rt_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {

@@ -103,7 +103,7 @@ EXPORTS = [
     "rt_destroy", "rt_render", "rt_render_device", "rt_unpermute_bands_device", "rt_intersect", "rt_shade",
     "rt_set_counting", "rt_debug_counters", "rt_ctx_info", "rt_selftest_math",
     "rt_postprocess_device", "rt_bitmap_device", "rt_postprocess", "rt_bitmap", "rt_encode_bmp", "rt_write_bmp",
-    "rt_philox4x32_10",
+    "rt_philox4x32_10", "rt_debug_wave_trace",
 ]
 
 class rt_post_params(C.Structure):
@@ -201,6 +201,7 @@ def lib():
             "rt_encode_bmp": ([C.c_int, C.c_int, P(C.c_uint8), P(C.c_uint8), C.c_long], C.c_long),
             "rt_write_bmp": ([C.c_char_p, C.c_int, C.c_int, P(C.c_uint8)], C.c_int),
             "rt_philox4x32_10": ([P(C.c_uint32), P(C.c_uint32), P(C.c_uint32)], C.c_int),
+            "rt_debug_wave_trace": ([vp, P(C.c_uint64), C.c_int], C.c_int),
         }
         for name, (args, res) in sigs.items():
             f = getattr(L, name)

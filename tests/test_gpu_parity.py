@@ -185,6 +185,9 @@ KERNEL_VARIANTS = [
     {"RT_KERNEL": "persistent"},
     {"RT_KERNEL": "df"},
     {"RT_KERNEL": "df", "RT_LEAFBATCH": "64"},
+    {"RT_KERNEL": "df", "RT_COOP": "0"},          # no cooperative drain traversal
+    {"RT_KERNEL": "df", "RT_COOP_MAX": "1"},      # drain groups of 64 lanes only
+    {"RT_KERNEL": "df", "RT_SCHED": "2"},         # cost-ordered job hand-out
     {"RT_KERNEL": "wavefront"},
     {"RT_KERNEL": "tile"},
     {"RT_KERNEL": "persistent", "RT_PACKET": "1"},

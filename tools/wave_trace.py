@@ -1,0 +1,54 @@
+"""Developer tool: per-wave timeline of the persistent render kernel (RT_WAVE_TRACE=1) -- launch
+skew, when each wave found the job queue empty, and what it did until it retired (drain
+iterations, tracing lanes per iteration, state-machine passes).
+Usage: python tools/wave_trace.py C3 [C4 ...]"""
+import ctypes as C
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "raytracer-group27_amd"))
+import numpy as np  # noqa: E402
+
+import rt_amd as R  # noqa: E402
+
+os.environ["RT_WAVE_TRACE"] = "1"
+Q = [0, 1, 5, 25, 50, 75, 95, 99, 100]
+
+
+def pct(x):
+    return " ".join(f"{v:.1f}" for v in np.percentile(x, Q))
+
+
+for cfg in [a for a in sys.argv[1:] if a.startswith("C")] or ["C3"]:
+    s, p, W, H, desc = R.build_config(cfg)
+    ctx = R.Context(s)
+    cam = R.camera_from_trackball(aspect=R.aspect_of(W, H))
+    ctx.render(cam, p, W, H)
+    _, st = ctx.render(cam, p, W, H)
+    buf = np.zeros(8 * 65536, np.uint64)
+    n = R.lib().rt_debug_wave_trace(ctx.h, buf.ctypes.data_as(C.POINTER(C.c_uint64)), 65536)
+    t = buf[:8 * n].reshape(n, 8).astype(np.int64)
+    t0 = t[:, 0].min()
+    start, end = (t[:, 0] - t0) / 100.0, (t[:, 1] - t0) / 100.0  # us
+    print(f"{cfg}: waves={n} kernel_ms={st.kernel_ms:.3f} span_us={end.max():.1f}", flush=True)
+    print("  start us pct " + pct(start))
+    print("  end   us pct " + pct(end))
+    print(f"  mean lifetime / span = {(end - start).mean() / end.max():.3f}; jobs/wave pct "
+          + " ".join(f"{x:.0f}" for x in np.percentile(t[:, 2], [0, 50, 100])))
+    dr = t[:, 3] > 0
+    if dr.any():
+        exh = (t[dr, 3] - t0) / 100.0
+        drain = end[dr] - exh
+        it = np.maximum(t[dr, 4], 1)
+        print("  queue dry us pct " + pct(exh))
+        print("  drain us pct     " + pct(drain))
+        print("  drain iters pct  " + pct(t[dr, 4]))
+        print("  lanes/iter pct   " + pct(t[dr, 5] / it))
+        print("  us/iter pct      " + pct(drain / it))
+        print("  drain phase-A passes pct " + pct(t[dr, 7]))
+        last = np.argsort(end)[-5:]
+        for i in last:
+            print(f"   last wave {i}: end {end[i]:.1f} dry {(t[i, 3] - t0) / 100.0:.1f} iters {t[i, 4]} "
+                  f"lanes/iter {t[i, 5] / max(1, t[i, 4]):.1f} phaseA {t[i, 7]}")
+    ctx.close()
