@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2  /* 2: textures (rt_texture, rt_params texture fields) */
 
 /* status codes */
 #define RT_OK 0
@@ -50,9 +50,22 @@ typedef struct rt_material {
     float ks[3];
     float shininess;
     float transparency;
-    int has_texture; /* kdTexture.has_value(); textures are off in the render path (main.cpp:58) */
-    int pad_;
+    int has_texture; /* kdTexture.has_value() */
+    int texture;     /* index into rt_scene_desc.textures when has_texture, else ignored */
 } rt_material;
+
+/* Decoded kd texture, what Image::Image (src/image.cpp:37-73) gets from
+ * stbi_load(path, &w, &h, &numChannels, STBI_rgb): `rgb` holds width*height*3 bytes and
+ * `channels` is the file's channel count.  rt_create turns it into texels the way the reference
+ * does -- texel k = rgb[k*channels + 0..2] / 255.0f (bytes past the buffer, which the reference
+ * reads for 4-channel files, are taken as 0) -- and builds the mip chain (src/image.cpp:408-452)
+ * for square power-of-two sizes.  channels < 3 is an error, as in the reference. */
+typedef struct rt_texture {
+    int width, height;
+    int channels;
+    int pad_;
+    const uint8_t* rgb;
+} rt_texture;
 
 /* Sphere, src/scene.h:48-53 */
 typedef struct rt_sphere {
@@ -91,6 +104,8 @@ typedef struct rt_scene_desc {
     const rt_spot_light* spot_lights;
     int num_plane_lights;
     const rt_plane_light* plane_lights;
+    int num_textures;
+    const rt_texture* textures;
 } rt_scene_desc;
 
 /*
@@ -118,7 +133,25 @@ typedef struct rt_params {
     int sample_size;              /* [4]: 4, 16 or 64 */
     int barycentric_mode;         /* 0 = "unthresholded" (defined semantics for the reference's UB) */
     uint64_t rng_seed;            /* glossy_ray_count > 1: Philox-4x32 stream seed (replaces rand()) */
+    /* kd textures (src/main.cpp:54-58,155-171; src/image.cpp:77-110) */
+    int use_textures;             /* [0] useTextures */
+    int texture_filtering;        /* [RT_TEX_NEAREST] textureFiltering (TextureFiltering, src/image.h) */
+    int out_of_bounds_x;          /* [RT_OOB_BORDER] outOfBoundsRuleX */
+    int out_of_bounds_y;          /* [RT_OOB_BORDER] outOfBoundsRuleY */
+    float border_color[3];        /* [0] textureBorderColor */
+    int pad_;
 } rt_params;
+
+/* TextureFiltering (src/image.h:22-29) */
+#define RT_TEX_NEAREST 0
+#define RT_TEX_BILINEAR 1
+#define RT_TEX_MIP_NEAREST 2          /* MipMappingNearestLevelNearestNeighbor */
+#define RT_TEX_MIP_NEAREST_BILINEAR 3 /* MipMappingNearestLevelBilinear */
+#define RT_TEX_TRILINEAR 4
+/* OutOfBoundsRule (src/image.h:16-20) */
+#define RT_OOB_BORDER 0
+#define RT_OOB_CLAMP 1
+#define RT_OOB_REPEAT 2
 
 /* Ray, framework/include/ray.h:11-15 (origin, direction, t{FLT_MAX}) */
 typedef struct rt_ray {
@@ -155,6 +188,12 @@ typedef struct rt_ctx rt_ctx;
 typedef struct rt_scene rt_scene;
 
 int rt_abi_version(void);
+/* PNG decoding with stbi_load(..., STBI_rgb) semantics (the texture loader of Image::Image,
+ * src/image.cpp:45): 8-bit RGB out, `channels` = the file's channel count as stb reports it
+ * (1 grey, 2 grey+alpha, 3 RGB or palette, 4 RGBA or palette with tRNS).  Call with rgb = NULL to
+ * get the size; rgb_size must then be >= width*height*3.  Non-interlaced PNG only. */
+int rt_decode_png(const uint8_t* data, long size, int* width, int* height, int* channels, uint8_t* rgb,
+                  long rgb_size);
 int rt_last_error(char* buf, size_t len);
 
 /* ---- scene ingest (host) ---- */

@@ -73,6 +73,98 @@ struct Mat {
     V3 kd, ks;
     float shininess = 1.0f;
     float transparency = 1.0f;
+    int texture = -1;  // kdTexture: index into Scene::images
+};
+
+// ---------------------------------------------------------------- Image (src/image.cpp)
+// The reference's texture: pixels from the stb RGB buffer (stepping by the file's channel
+// count, :57-59), the mip chain of square power-of-two images (:408-452), getPixel and its
+// filters (:77-360), level choice (:500-540).
+struct Image {
+    int w = 0, h = 0;
+    bool mip = false;
+    std::vector<std::vector<V3>> levels;  // _mipmap[0] = m_pixels
+
+    Image(const rt_texture& t) : w(t.width), h(t.height) {
+        const size_t nbytes = (size_t)w * h * 3;
+        std::vector<V3> px;
+        for (size_t i = 0; i < (size_t)w * h * t.channels; i += t.channels) {
+            auto at = [&](size_t j) { return j < nbytes ? (float)t.rgb[j] : 0.0f; };
+            px.emplace_back(at(i) / 255.0f, at(i + 1) / 255.0f, at(i + 2) / 255.0f);
+        }
+        levels.push_back(px);
+        mip = ((h & (h - 1)) == 0) && ((w & (w - 1)) == 0) && (w == h);
+        if (!mip) return;
+        for (int k = w; k > 1; k /= 2) {
+            const int r = k / 2;
+            const std::vector<V3>& o = levels.back();
+            std::vector<V3> red((size_t)r * r);
+            for (int x = 0, rx = 0; x + 1 < k && rx < r; x += 2, rx++)
+                for (int y = 0, ry = 0; y + 1 < k && ry < r; y += 2, ry++)
+                    red[(size_t)ry * r + rx] = 0.25f * (o[(size_t)y * k + x] + o[(size_t)(y + 1) * k + x] +
+                                                        o[(size_t)y * k + x + 1] + o[(size_t)(y + 1) * k + x + 1]);
+            levels.push_back(red);
+        }
+    }
+    int lw(int l) const { return w >> l; }
+    int lh(int l) const { return h >> l; }
+    static bool out(float c) { return c < 0 || c > 1; }
+    static float wrap(float c, int rule) {
+        if (rule == RT_OOB_CLAMP) return c > 1 ? 1.0f : (c < 0 ? 0.0f : c);
+        if (rule == RT_OOB_REPEAT && out(c)) return c - std::floor(c);
+        return c;
+    }
+    void to_image(float u, float v, int l, float& x, float& y) const {
+        x = u * (unsigned)(lw(l) - 1);
+        y = (1.0f - v) * (unsigned)(lh(l) - 1);
+    }
+    V3 nearest(float fx, float fy, int l) const {
+        unsigned x = (unsigned)std::round(fx), y = (unsigned)std::round(fy);
+        if (x >= (unsigned)lw(l)) x = lw(l) - 1;
+        if (y >= (unsigned)lh(l)) y = lh(l) - 1;
+        return levels[l][(size_t)y * lw(l) + x];
+    }
+    static V3 lerp(float lo, float hi, const V3& cl, const V3& ch, float p) {
+        if (std::fabs(hi - lo) < 1e-6) return cl;
+        const float c = (p - lo) / (hi - lo);
+        return (1 - c) * cl + c * ch;
+    }
+    V3 bilinear(float fx, float fy, int l) const {
+        const float x0 = std::floor(fx), x1 = std::ceil(fx), y0 = std::floor(fy), y1 = std::ceil(fy);
+        auto at = [&](float x, float y) { return levels[l][(size_t)(unsigned)y * lw(l) + (unsigned)x]; };
+        const V3 lo = lerp(x0, x1, at(x0, y0), at(x1, y0), fx);
+        const V3 hi = lerp(x0, x1, at(x0, y1), at(x1, y1), fx);
+        return lerp(y0, y1, lo, hi, fy);
+    }
+    int nlevels() const { return (int)levels.size(); }
+    V3 get_pixel(float u, float v, float lod, const rt_params& P) const {
+        const V3 border = V3::of(P.border_color);
+        if (P.out_of_bounds_x == RT_OOB_BORDER && out(u)) return border;
+        if (P.out_of_bounds_y == RT_OOB_BORDER && out(v)) return border;
+        const float iu = wrap(u, P.out_of_bounds_x), iv = wrap(v, P.out_of_bounds_y);
+        float x, y;
+        if (P.texture_filtering == RT_TEX_NEAREST || P.texture_filtering == RT_TEX_BILINEAR) {
+            to_image(iu, iv, 0, x, y);
+            return P.texture_filtering == RT_TEX_NEAREST ? nearest(x, y, 0) : bilinear(x, y, 0);
+        }
+        if (P.texture_filtering == RT_TEX_TRILINEAR) {
+            if (!mip) return V3(0.0f);
+            const int hi = (int)fmin_g(nlevels() - 1.0f, std::ceil(lod));
+            const int lo = (int)fmax_g(0.0f, std::floor(lod));
+            float xl, yl, xh, yh;
+            to_image(iu, iv, lo, xl, yl);
+            to_image(iu, iv, hi, xh, yh);
+            return lerp((float)lo, (float)hi, bilinear(xl, yl, lo), bilinear(xh, yh, hi), lod);
+        }
+        if (!mip) return V3(1.0f);
+        unsigned best;
+        if (lod - std::floor(lod) < std::ceil(lod) - lod)
+            best = (int)fmax_g(0.0f, std::floor(lod));
+        else
+            best = (int)fmin_g(nlevels() - 1.0f, std::ceil(lod));
+        to_image(iu, iv, (int)best, x, y);
+        return P.texture_filtering == RT_TEX_MIP_NEAREST ? nearest(x, y, (int)best) : bilinear(x, y, (int)best);
+    }
 };
 struct Vert {
     V3 p, n;
@@ -119,6 +211,7 @@ struct Scene {
     std::vector<rt_spot_light> spots;
     std::vector<rt_plane_light> planes;
     std::vector<Node> nodes;
+    std::vector<Image> images;
 };
 
 // ---------------------------------------------------------------- primitives (ray_tracing.cpp)
@@ -551,12 +644,56 @@ static V3 phong(const Light& l, const Mat& m) {
 }
 
 // ---------------------------------------------------------------- getFinalColor (main.cpp:129-301)
+// Ray differentials (framework/include/ray.h:17-28, src/ray_differentials.cpp) with the values
+// the member initialisers intend (right = (1,0,0), up = (0,-1,0); the reference reads them
+// before they are initialised): a camera ray is default-constructed (direction (0,0,-1)) and
+// set afterwards, a secondary ray is aggregate-initialised with its direction.  Only the
+// transferred dP reaches the level of detail.
+static float level_of_detail(const Ray& ray, bool camera_ray, const Hit& h, const std::array<Vert, 3>& tv) {
+    const V3 right(1.0f, 0.0f, 0.0f), up(0.0f, -1.0f, 0.0f);
+    const V3 dir0 = camera_ray ? V3(0.0f, 0.0f, -1.0f) : ray.direction;
+    const V3 dD_dx = (vdot(dir0, dir0) * right - vdot(dir0, right) * dir0) / std::pow(vdot(dir0, dir0), 1.5f);
+    const V3 dD_dy = (vdot(dir0, dir0) * up - vdot(dir0, up) * dir0) / std::pow(vdot(dir0, dir0), 1.5f);
+    V3 dP_dx(0.0f), dP_dy(0.0f);
+    // transfer_ray_differentials (:5-15)
+    const V3 N = vnormalize(h.normal), D = vnormalize(ray.direction);
+    const float dt_dx = -vdot(dP_dx + ray.t * dD_dx, N) / vdot(D, N);
+    const float dt_dy = -vdot(dP_dy + ray.t * dD_dy, N) / vdot(D, N);
+    dP_dx = (dP_dx + ray.t * dD_dx) + dt_dx * D;
+    dP_dy = (dP_dy + ray.t * dD_dy) + dt_dy * D;
+    // computeDerivativeOfBarycentricCoordinate (:36-45), computeTexturePartialDerivative... (:66-80)
+    auto dbary = [](const V3& a, const V3& b, const V3& p, const V3& pd, float area) {
+        const V3 term1 = vcross(pd, p - b) + vcross(p - a, pd);
+        const V3 term2 = vcross(a - p, b - p);
+        return (vdot(term1, term2) + vdot(term2, term1)) / (2 * area * std::sqrt(vdot(term2, term2)));
+    };
+    auto dT = [&](const V3& pd, float& du, float& dv) {
+        const float area = vlength(vcross(tv[2].p - tv[0].p, tv[1].p - tv[0].p));
+        const float a = dbary(tv[2].p, tv[1].p, h.hitPoint, pd, area);
+        const float b = dbary(tv[0].p, tv[2].p, h.hitPoint, pd, area);
+        const float g = dbary(tv[1].p, tv[0].p, h.hitPoint, pd, area);
+        du = (a * tv[0].u + b * tv[1].u) + g * tv[2].u;
+        dv = (a * tv[0].v + b * tv[1].v) + g * tv[2].v;
+    };
+    float ux, vx, uy, vy;
+    dT(1.0f * dP_dx, ux, vx);
+    dT(1.0f * dP_dy, uy, vy);
+    const float lx = std::sqrt(ux * ux + vx * vx), ly = std::sqrt(uy * uy + vy * vy);
+    return fmax_g(0.0f, std::log2(fmax_g(lx, ly)));  // computeLevelOfDetails (:112-139)
+}
+
 static V3 final_color(Scene& sc, const rt_params& P, Ray ray, int level, Counter& cnt) {
     Hit h;
     if (!intersect(sc, ray, h, P.use_bvh != 0, cnt)) return V3(0.0f);
     V3 color(0.0f);
     const V3 refl = vreflect(vnormalize(ray.direction), vnormalize(h.normal));
-    const Mat m = h.material(sc.mats);
+    Mat m = h.material(sc.mats);
+    // matForRendering.kd from the texture (src/main.cpp:146-171)
+    if (P.use_textures && h.is_triangle && m.texture >= 0) {
+        const auto& tv = sc.tris[h.prim];
+        const float lod = P.texture_filtering >= RT_TEX_MIP_NEAREST ? level_of_detail(ray, level == 0, h, tv) : 0.0f;
+        m.kd = sc.images[m.texture].get_pixel(h.u, h.v, lod, P);
+    }
     std::vector<Light> lights;
     gather_lights(sc, h, refl, P, lights, cnt);
     for (const Light& l : lights) color += phong(l, m);
@@ -722,8 +859,11 @@ oracle_scene* oracle_create(const rt_scene_desc* d) {
         mm.ks = V3::of(d->materials[m].ks);
         mm.shininess = d->materials[m].shininess;
         mm.transparency = d->materials[m].transparency;
+        if (d->materials[m].has_texture && d->materials[m].texture >= 0 && d->materials[m].texture < d->num_textures)
+            mm.texture = d->materials[m].texture;
         sc.mats.push_back(mm);
     }
+    for (int t = 0; t < d->num_textures; ++t) sc.images.emplace_back(d->textures[t]);
     for (int t = 0; t < d->num_triangles; ++t) {
         std::array<Vert, 3> tri;
         for (int c = 0; c < 3; ++c) {

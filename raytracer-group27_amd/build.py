@@ -12,7 +12,7 @@ CSRC = os.path.join(HERE, "csrc")
 BUILD = os.path.join(HERE, "build")
 LIB = os.path.join(HERE, "librt_amd.so")
 
-HOST_SRCS = ["obj_loader.cpp", "scene.cpp", "bvh_build.cpp", "rt_api_host.cpp", "bmp.cpp"]
+HOST_SRCS = ["obj_loader.cpp", "scene.cpp", "bvh_build.cpp", "rt_api_host.cpp", "bmp.cpp", "png_decode.cpp"]
 HIP_SRCS = ["rt_runtime.hip", "rt_post.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("RT_OFFLOAD_ARCH", "gfx950")
@@ -52,7 +52,7 @@ def build(force=False, verbose_resource=False):
                  + extra + ["-c", src, "-o", obj])
         objs.append(obj)
     if force or not os.path.exists(LIB) or any(os.path.getmtime(o) > os.path.getmtime(LIB) for o in objs):
-        _run([HIPCC, "-shared", "-fPIC", "-o", LIB] + objs)
+        _run([HIPCC, "-shared", "-fPIC", "-o", LIB] + objs + ["-lz"])
     return LIB
 
 

@@ -24,6 +24,14 @@ struct Material {
     float transparency = 1.0f;
     bool has_texture = false;
     std::string texture_path;
+    int texture = -1;  // index into HostScene::textures once loaded
+};
+
+// Image (src/image.h): the decoded file as stbi_load(..., STBI_rgb) returns it
+struct HostTexture {
+    std::string path;
+    int width = 0, height = 0, channels = 0;
+    std::vector<uint8_t> rgb;
 };
 
 struct Mesh {
@@ -40,10 +48,16 @@ struct HostScene {
     std::vector<rt_spot_light> spot_lights;
     std::vector<rt_plane_light> plane_lights;
 
+    std::vector<HostTexture> textures;
+    // Image::Image for every mesh with a kd texture not yet loaded (src/mesh.cpp:141): throws
+    // std::runtime_error when the file is missing, undecodable or has fewer than 3 channels
+    void load_textures();
+
     // flattened view (rebuilt by flatten())
     std::vector<float> flat_pos, flat_nrm, flat_uv;
     std::vector<int> flat_mesh;
     std::vector<rt_material> flat_mat;
+    std::vector<rt_texture> flat_tex;
     void flatten();
     void fill_desc(rt_scene_desc* d) const;
 };

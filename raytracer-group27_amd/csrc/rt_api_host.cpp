@@ -62,6 +62,7 @@ extern "C" int rt_scene_load_obj(rt_scene* sc, const char* path, int normalize, 
         auto meshes = load_obj(path, normalize != 0, x4 != 0);
         for (auto& m : meshes) sc->s.meshes.push_back(std::move(m));
         sc->dirty = true;
+        sc->s.load_textures();
         return RT_OK;
     }
     CATCH_ALL(RT_ERR_IO)
@@ -75,6 +76,7 @@ extern "C" int rt_scene_preset(rt_scene* sc, int preset, const char* data_dir, i
     try {
         load_preset(sc->s, preset, data_dir, x4 != 0);
         sc->dirty = true;
+        sc->s.load_textures();
         return RT_OK;
     }
     CATCH_ALL(RT_ERR_IO)
@@ -124,6 +126,7 @@ extern "C" int rt_scene_set_material(rt_scene* sc, int mesh, const rt_material* 
     d.shininess = m->shininess;
     d.transparency = m->transparency;
     d.has_texture = m->has_texture != 0;
+    d.texture = m->has_texture ? m->texture : -1;
     sc->dirty = true;
     return RT_OK;
 }

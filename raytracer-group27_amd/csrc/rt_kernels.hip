@@ -67,6 +67,15 @@ struct DevScene {
     int ntri, nsph, nref;
     int npl, nsl, nspot, nplane;
     int all_opaque;  // every mesh and sphere material has transparency == 1.0f
+    // kd textures (Image, src/image.cpp): texels (r, g, b) of every level of every texture;
+    // per texture (level-0 texel offset, width, height, mip levels or 0); per mesh texture or -1
+    const float* __restrict__ tex;
+    const int4* __restrict__ tex_info;
+    const int* __restrict__ mat_tex;
+    int ntex;
+    // per render (rt_params): useTextures, textureFiltering, outOfBoundsRuleX/Y, textureBorderColor
+    int tex_on, tex_filter, tex_oob_x, tex_oob_y;
+    float tex_border[3];
 };
 
 struct KParams {
@@ -398,7 +407,135 @@ struct Surf {
     bool is_tri;
 };
 
-__device__ __forceinline__ Surf surface(const DevScene& S, v3 o, v3 d, const Best& b) {
+// ------------------------------------------------------------------------------------------
+// kd textures: Image::getPixel (src/image.cpp:77-110) and its filters (:200-360), with the level
+// of detail of computeLevelOfDetails (src/ray_differentials.cpp:112-139).
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ v3 tex_texel(const DevScene& S, int4 ti, int level, uint32_t x, uint32_t y) {
+    size_t off = (size_t)ti.x;
+    for (int l = 0; l < level; ++l) off += (size_t)(ti.y >> l) * (size_t)(ti.z >> l);
+    const float* p = S.tex + 3 * (off + (size_t)y * (uint32_t)(ti.y >> level) + x);
+    return v3{p[0], p[1], p[2]};
+}
+
+// toImageCoordinates (:114-130)
+__device__ __forceinline__ v2 tex_image_coords(int4 ti, v2 tc, int level) {
+    const uint32_t w = (uint32_t)(ti.y >> level), h = (uint32_t)(ti.z >> level);
+    return v2{tc.x * (float)(w - 1u), (1.0f - tc.y) * (float)(h - 1u)};
+}
+
+// nearestNeighbor (:201-229): round, clamp to the last row / column
+__device__ __forceinline__ v3 tex_nearest(const DevScene& S, int4 ti, v2 ic, int level) {
+    const uint32_t w = (uint32_t)(ti.y >> level), h = (uint32_t)(ti.z >> level);
+    uint32_t x = (uint32_t)roundf(ic.x), y = (uint32_t)roundf(ic.y);
+    if (x >= w) x = w - 1u;
+    if (y >= h) y = h - 1u;
+    return tex_texel(S, ti, level, x, y);
+}
+
+// linearInterpolation (:329-339)
+__device__ __forceinline__ v3 tex_lerp(float lo, float hi, v3 cl, v3 ch, float p) {
+    if ((double)fabsf(hi - lo) < 1e-6) return cl;
+    const float c = (p - lo) / (hi - lo);
+    return (1.0f - c) * cl + c * ch;
+}
+
+// bilinearInterpolation (:232-252)
+__device__ __forceinline__ v3 tex_bilinear(const DevScene& S, int4 ti, v2 ic, int level) {
+    const float xl = floorf(ic.x), xh = ceilf(ic.x), yl = floorf(ic.y), yh = ceilf(ic.y);
+    const v3 c_ll = tex_texel(S, ti, level, (uint32_t)xl, (uint32_t)yl);
+    const v3 c_lr = tex_texel(S, ti, level, (uint32_t)xh, (uint32_t)yl);
+    const v3 c_hl = tex_texel(S, ti, level, (uint32_t)xl, (uint32_t)yh);
+    const v3 c_hr = tex_texel(S, ti, level, (uint32_t)xh, (uint32_t)yh);
+    const v3 lo = tex_lerp(xl, xh, c_ll, c_lr, ic.x);
+    const v3 hi = tex_lerp(xl, xh, c_hl, c_hr, ic.x);
+    return tex_lerp(yl, yh, lo, hi, ic.y);
+}
+
+// clampRepeatTextureCoordinate (:133-191)
+__device__ __forceinline__ float tex_wrap(float c, int rule) {
+    if (rule == RT_OOB_CLAMP) return c > 1.0f ? 1.0f : (c < 0.0f ? 0.0f : c);
+    if (rule == RT_OOB_REPEAT && (c < 0.0f || c > 1.0f)) return c - floorf(c);
+    return c;
+}
+
+// getPixel (:77-110); levels per getBestLevelMipmap (:500-540)
+__device__ v3 tex_get_pixel(const DevScene& S, int t, v2 tc, float lod) {
+    if (S.tex_oob_x == RT_OOB_BORDER && (tc.x < 0.0f || tc.x > 1.0f))
+        return v3{S.tex_border[0], S.tex_border[1], S.tex_border[2]};
+    if (S.tex_oob_y == RT_OOB_BORDER && (tc.y < 0.0f || tc.y > 1.0f))
+        return v3{S.tex_border[0], S.tex_border[1], S.tex_border[2]};
+    const v2 in{tex_wrap(tc.x, S.tex_oob_x), tex_wrap(tc.y, S.tex_oob_y)};
+    const int4 ti = S.tex_info[t];
+    const int f = S.tex_filter;
+    if (f == RT_TEX_NEAREST) return tex_nearest(S, ti, tex_image_coords(ti, in, 0), 0);
+    if (f == RT_TEX_BILINEAR) return tex_bilinear(S, ti, tex_image_coords(ti, in, 0), 0);
+    const int nlev = ti.w;
+    if (f == RT_TEX_TRILINEAR) {
+        if (nlev == 0) return v3{0.0f, 0.0f, 0.0f};
+        const int hi = (int)gmin((float)nlev - 1.0f, ceilf(lod));
+        const int lo = (int)gmax(0.0f, floorf(lod));
+        const v3 cl = tex_bilinear(S, ti, tex_image_coords(ti, in, lo), lo);
+        const v3 ch = tex_bilinear(S, ti, tex_image_coords(ti, in, hi), hi);
+        return tex_lerp((float)lo, (float)hi, cl, ch, lod);
+    }
+    if (nlev == 0) return v3{1.0f, 1.0f, 1.0f};
+    const int best = (lod - floorf(lod) < ceilf(lod) - lod) ? (int)gmax(0.0f, floorf(lod))
+                                                           : (int)gmin((float)nlev - 1.0f, ceilf(lod));
+    const v2 ic = tex_image_coords(ti, in, best);
+    return f == RT_TEX_MIP_NEAREST ? tex_nearest(S, ti, ic, best) : tex_bilinear(S, ti, ic, best);
+}
+
+// computeDerivativeOfBarycentricCoordinate (src/ray_differentials.cpp:36-45)
+__device__ __forceinline__ float tex_dbary(v3 a, v3 b, v3 p, v3 pd, float area) {
+    const v3 term1 = cross(pd, p - b) + cross(p - a, pd);
+    const v3 term2 = cross(a - p, b - p);
+    const float nom = dot(term1, term2) + dot(term2, term1);
+    const float den = 2.0f * area * sqrtf(dot(term2, term2));
+    return nom / den;
+}
+
+// computeTexturePartialDerivativeInInterpolatedTrianglePoint (:66-80)
+__device__ __forceinline__ v2 tex_dT(v3 v0, v3 v1, v3 v2p, v2 t0, v2 t1, v2 t2, v3 p, v3 pd) {
+    const float area = length(cross(v2p - v0, v1 - v0));
+    const float a = tex_dbary(v2p, v1, p, pd, area);
+    const float b = tex_dbary(v0, v2p, p, pd, area);
+    const float g = tex_dbary(v1, v0, p, pd, area);
+    return v2{(a * t0.x + b * t1.x) + g * t2.x, (a * t0.y + b * t1.y) + g * t2.y};
+}
+
+// Level of detail of a triangle hit: the ray's differentials as Ray's member initialisers give
+// them (right = (1,0,0), up = (0,-1,0); a camera ray is default-constructed with direction
+// (0,0,-1) and set afterwards, a secondary ray is built with its direction), transferred to the
+// hit (transfer_ray_differentials, :5-15), then computeLevelOfDetails (:112-139).  The reference
+// reads `right`/`up` before their initialisers run (ray.h:19-20 vs :25-28); this is the value
+// the initialisers intend.
+__device__ float tex_lod(v3 d, float t, v3 normal, bool primary, v3 v0, v3 v1, v3 v2p, v2 t0, v2 t1, v2 t2,
+                         v3 p) {
+    const v3 right{1.0f, 0.0f, 0.0f}, up{0.0f, -1.0f, 0.0f};
+    const v3 dc = primary ? v3{0.0f, 0.0f, -1.0f} : d;
+    const float dd = dot(dc, dc);
+    const float pw = powf(dd, 1.5f);
+    const v3 dDx = (dd * right - dot(dc, right) * dc) / pw;
+    const v3 dDy = (dd * up - dot(dc, up) * dc) / pw;
+    const v3 N = normalize(normal), D = normalize(d);
+    const v3 zero{0.0f, 0.0f, 0.0f};
+    const v3 ax = zero + t * dDx, ay = zero + t * dDy;
+    const float dtx = -dot(ax, N) / dot(D, N);
+    const float dty = -dot(ay, N) / dot(D, N);
+    const v3 dPx = ax + dtx * D, dPy = ay + dty * D;
+    const v2 dTx = tex_dT(v0, v1, v2p, t0, t1, t2, p, 1.0f * dPx);
+    const v2 dTy = tex_dT(v0, v1, v2p, t0, t1, t2, p, 1.0f * dPy);
+    const float lx = sqrtf(dTx.x * dTx.x + dTx.y * dTx.y), ly = sqrtf(dTy.x * dTy.x + dTy.y * dTy.y);
+    const float m = (lx < ly) ? ly : lx;  // glm::max
+    const float l2 = log2f(m);
+    return (0.0f < l2) ? l2 : 0.0f;
+}
+
+// shade = the hit is shaded (getFinalColor): a textured triangle's kd comes from its texture
+// (src/main.cpp:155-171); primary = the ray is a camera ray (level 0)
+__device__ __forceinline__ Surf surface(const DevScene& S, v3 o, v3 d, const Best& b, bool shade = false,
+                                        bool primary = false) {
     Surf s;
     if (b.rec >= 0) {
         const float4* tp = S.tri + b.rec * 4;
@@ -426,6 +563,19 @@ __device__ __forceinline__ Surf surface(const DevScene& S, v3 o, v3 d, const Bes
         s.m = S.mats[s.mesh];
         s.prim = sidx;
         s.is_tri = true;
+        if (shade && S.tex_on) {
+            const int tx = S.mat_tex[s.mesh];
+            if (tx >= 0) {
+                float lod = 0.0f;
+                if (S.tex_filter >= RT_TEX_MIP_NEAREST)
+                    lod = tex_lod(d, b.t, s.n, primary, v0, v1, v2, rt::v2{uu[0], uu[1]}, rt::v2{uu[2], uu[3]},
+                                  rt::v2{uu[4], uu[5]}, s.p);
+                const v3 kd = tex_get_pixel(S, tx, s.uv, lod);
+                s.m.kd[0] = kd.x;
+                s.m.kd[1] = kd.y;
+                s.m.kd[2] = kd.z;
+            }
+        }
     } else {
         const int si = -b.rec - 1;
         const DSph sp = S.sph[si];
@@ -619,6 +769,7 @@ struct Frame {
     // direction, shininess and the lobe half-width d (host-evaluated per material)
     v3 hp, nraw, sdir;
     float shin, gd;
+    v3 kd;  // persistent kernels: kd of the shading point at this level (texture or material)
 };
 
 template <bool COUNT>
@@ -637,7 +788,7 @@ __device__ v3 get_final_color(const KParams& P, v3 o, v3 d, float t_init, int* s
         t_init = FLT_MAX;
         if (hit) {
             if (COUNT) cnt.hits++;
-            const Surf s = surface(S, o, d, b);
+            const Surf s = surface(S, o, d, b, true, level == 0);
             const v3 refl = reflect(normalize(d), normalize(s.n));
             col = direct_light<COUNT>(P, s, refl, stk, cnt);
             if (level < P.max_level) {

@@ -53,6 +53,20 @@ __device__ __forceinline__ DMat load_mat(const DevScene& S, int m) {
     return S.sph[-m - 1].m;
 }
 
+// matForRendering (src/main.cpp:146-171): the shading point's material with its kd, which
+// surface() took from the texture when there is one; kept in the level's frame (scratch), not
+// in the lane's registers
+template <bool TEX>
+__device__ __forceinline__ DMat render_mat(const DevScene& S, const Lane& L, const Frame* fr) {
+    DMat m = load_mat(S, L.mat);
+    if (!TEX) return m;
+    const v3 kd = fr[L.level].kd;
+    m.kd[0] = kd.x;
+    m.kd[1] = kd.y;
+    m.kd[2] = kd.z;
+    return m;
+}
+
 // Traversal with run-time mode flags: one instance serves every query type.
 template <bool COUNT>
 __device__ __forceinline__ bool trace_query(const DevScene& S, v3 o, v3 d, float t_init, float thr, bool REF, bool ANY,
@@ -389,7 +403,8 @@ __device__ __forceinline__ v3 sphere_perp(const Lane& L, v3 lp, float radius) {
 
 // Advance the light loop until a shadow query is needed (true) or all lights are done (false).
 // `vis` carries the result of the cansee that just finished (valid when have_result).
-__device__ bool advance_lights(const KParams& P, Lane& L, bool have_result, bool vis) {
+template <bool TEX>
+__device__ bool advance_lights(const KParams& P, Lane& L, const Frame* fr, bool have_result, bool vis) {
     const DevScene& S = P.S;
     for (;;) {
         if (L.lt == L_POINT) {
@@ -399,7 +414,7 @@ __device__ bool advance_lights(const KParams& P, Lane& L, bool have_result, bool
                     const rt_point_light pl = S.pl[L.li];
                     float cosL, cosS;
                     light_cos(L, ld3(pl.position), cosL, cosS);
-                    L.color += calc_color(ld3(pl.color), L.sI, cosL, cosS, load_mat(S, L.mat));
+                    L.color += calc_color(ld3(pl.color), L.sI, cosL, cosS, render_mat<TEX>(S, L, fr));
                 }
                 L.li++;
             }
@@ -446,7 +461,7 @@ __device__ bool advance_lights(const KParams& P, Lane& L, bool have_result, bool
                 if (L.a1 > 0.0f) {
                     float cosL, cosS;
                     light_cos(L, lp, cosL, cosS);
-                    L.color += calc_color(ld3(sl.color), L.a0 / (float)P.sl_count, cosL, cosS, load_mat(S, L.mat));
+                    L.color += calc_color(ld3(sl.color), L.a0 / (float)P.sl_count, cosL, cosS, render_mat<TEX>(S, L, fr));
                 }
                 L.li++;
                 L.ls = -1;
@@ -470,7 +485,7 @@ __device__ bool advance_lights(const KParams& P, Lane& L, bool have_result, bool
                     const DSpot sp = S.spot[L.li];
                     float cosL, cosS;
                     light_cos(L, ld3(sp.pos), cosL, cosS);
-                    L.color += calc_color(ld3(sp.color), L.sI, cosL, cosS, load_mat(S, L.mat));
+                    L.color += calc_color(ld3(sp.color), L.sI, cosL, cosS, render_mat<TEX>(S, L, fr));
                 }
                 L.li++;
             }
@@ -537,7 +552,7 @@ __device__ bool advance_lights(const KParams& P, Lane& L, bool have_result, bool
             if (L.ls >= k * k) {
                 if (L.a0 > 0.0f) {
                     const float li = (L.a3 / (float)(int)L.a1) * L.a0 / (float)(k * k);
-                    L.color += calc_color(ld3(pl.color), li, 1.0f, L.a2, load_mat(S, L.mat));
+                    L.color += calc_color(ld3(pl.color), li, 1.0f, L.a2, render_mat<TEX>(S, L, fr));
                 }
                 L.li++;
                 L.ls = -1;
@@ -703,7 +718,13 @@ struct JobSrc {
     float* rgb;                    // mode 1 output [n][3]
     unsigned long long* ray_counts;  // mode 1 per-ray counts
     int* counter;                  // global job counter (zeroed per launch)
+    int* xq;  // dynamic-fetch kernel, or null: 8 job heads (32-int spacing, zeroed per launch), one
+              // per group of blocks sharing an XCD (blockIdx % 8), each over 1/8 of the jobs
 };
+
+// Job range of XCD group x: a contiguous run of 8x8 tiles (a horizontal band of the frame), so
+// the rays of one XCD touch the geometry of one band and its L2 holds that part of the scene.
+__device__ __forceinline__ int xq_lo(const JobSrc& J, int x) { return ((x * ((J.njobs + 63) >> 6)) >> 3) << 6; }
 
 // queue the camera ray of the lane's current sample (src/main.cpp:350-386)
 __device__ __forceinline__ void queue_camera(const KParams& P, Lane& L) {
@@ -755,7 +776,7 @@ __device__ __forceinline__ bool job_pixel(const KParams& P, int job, Lane& L) {
     return (L.px < P.W) && (row_in_band < P.band_rows) && (L.py < P.H) && (lb < P.n_local_bands);
 }
 
-template <bool COUNT, int WPE, int BW>
+template <bool COUNT, int WPE, int BW, bool TEX = true>
 __global__ __launch_bounds__(64, WPE) void persistent_kernel(KParams P, JobSrc J) {
     __shared__ int stack_lds[RT_STACK_SIZE * RT_WAVE];
     __shared__ int s_base;
@@ -900,13 +921,14 @@ __global__ __launch_bounds__(64, WPE) void persistent_kernel(KParams P, JobSrc J
                 node_hit = false;
             } else {
                 if (COUNT) cnt.hits++;
-                const Surf s = surface(S, L.qo, L.qd, b);
+                const Surf s = surface(S, L.qo, L.qd, b, TEX, L.level == 0);
                 L.hp = s.p;
                 L.nraw = s.n;
                 L.nN = normalize(s.n);
                 L.refl = reflect(normalize(L.qd), L.nN);
                 L.nR = normalize(L.refl);
                 L.mat = (b.rec >= 0) ? s.mesh : b.rec;
+            if (TEX) fr[L.level].kd = v3{s.m.kd[0], s.m.kd[1], s.m.kd[2]};
                 L.color = v3{0.0f, 0.0f, 0.0f};
                 L.lt = L_POINT;
                 L.li = 0;
@@ -914,7 +936,7 @@ __global__ __launch_bounds__(64, WPE) void persistent_kernel(KParams P, JobSrc J
                 run_lights = true;
             }
         }
-        if (run_lights && advance_lights(P, L, lights_have, lights_vis)) {
+        if (run_lights && advance_lights<TEX>(P, L, fr, lights_have, lights_vis)) {
             need_trace = true;
             continue;
         }
@@ -1437,7 +1459,7 @@ __device__ __forceinline__ void trav_finish(const DevScene& S, Trav& T) {
 // The state-machine advance of persistent_kernel after a finished query (shadow segment,
 // light loop, recursion fold, pixel output).  Returns true with the next query in L.q*; false
 // when the lane's job is complete (L.job = -1).
-template <bool COUNT>
+template <bool COUNT, bool TEX = true>
 __device__ bool advance_lane(const KParams& P, const JobSrc& J, Lane& L, Frame* fr, bool hit, const Best& b,
                              Cnt& cnt, const Cnt& job_cnt) {
     const DevScene& S = P.S;
@@ -1480,13 +1502,14 @@ __device__ bool advance_lane(const KParams& P, const JobSrc& J, Lane& L, Frame* 
             node_hit = false;
         } else {
             if (COUNT) cnt.hits++;
-            const Surf s = surface(S, L.qo, L.qd, b);
+            const Surf s = surface(S, L.qo, L.qd, b, TEX, L.level == 0);
             L.hp = s.p;
             L.nraw = s.n;
             L.nN = normalize(s.n);
             L.refl = reflect(normalize(L.qd), L.nN);
             L.nR = normalize(L.refl);
             L.mat = (b.rec >= 0) ? s.mesh : b.rec;
+            if (TEX) fr[L.level].kd = v3{s.m.kd[0], s.m.kd[1], s.m.kd[2]};
             L.color = v3{0.0f, 0.0f, 0.0f};
             L.lt = L_POINT;
             L.li = 0;
@@ -1494,7 +1517,7 @@ __device__ bool advance_lane(const KParams& P, const JobSrc& J, Lane& L, Frame* 
             run_lights = true;
         }
     }
-    if (run_lights && advance_lights(P, L, lights_have, lights_vis)) return true;
+    if (run_lights && advance_lights<TEX>(P, L, fr, lights_have, lights_vis)) return true;
     v3 out;
     if (finish_node(P, L, fr, node_hit, out)) return true;
     // level-0 colour complete
@@ -1524,12 +1547,12 @@ __device__ bool advance_lane(const KParams& P, const JobSrc& J, Lane& L, Frame* 
     return false;
 }
 
-template <bool COUNT, int WPE, int BW>
+template <bool COUNT, int WPE, int BW, bool TEX = true>
 __global__ __launch_bounds__(64, WPE) void persistent_df_kernel(KParams P, JobSrc J) {
     __shared__ int stack_lds[RT_STACK8 * RT_WAVE];
     __shared__ int coop_pool[COOP_POOL];   // drain: node groups of the wave's last queries
     __shared__ int coop_q[CQ_N * COOP_Q];  // drain: those queries
-    __shared__ int s_base;
+    __shared__ int s_base, s_lim;
     const int lane_id = threadIdx.x;
     int* stk = stack_lds + lane_id;
     const unsigned long long t_wave0 = P.wave_trace ? wall_clock64() : 0ull;
@@ -1541,6 +1564,7 @@ __global__ __launch_bounds__(64, WPE) void persistent_df_kernel(KParams P, JobSr
     Trav T;
     Cnt cnt{0u, 0u, 0u, 0u};
     Cnt job_cnt{0u, 0u, 0u, 0u};  // per-job ray count (rt_shade)
+    int xr = (int)(blockIdx.x & 7), xtried = 0;  // J.xq: the job range this wave draws from, ranges used up
     bool tracing = false;          // a query is in flight
     bool pending = false;          // a finished query waits for advance_lane
     const int refill_at = P.refill;
@@ -1556,19 +1580,33 @@ __global__ __launch_bounds__(64, WPE) void persistent_df_kernel(KParams P, JobSr
         if (pending) {
             pending = false;
             if (COUNT && wave_leader()) cnt.wadv++;
-            start = advance_lane<COUNT>(P, J, L, fr, T.found, T.best, cnt, job_cnt);
+            start = advance_lane<COUNT, TEX>(P, J, L, fr, T.found, T.best, cnt, job_cnt);
         }
         const bool idle = (L.job == -1);
         const unsigned long long want = __ballot(idle);
         if (want) {
-            if (lane_id == __ffsll((long long)want) - 1) s_base = atomicAdd(J.counter, __popcll(want));
-            wave_jobs += (unsigned int)__popcll(want);
+            const int nwant = __popcll(want);
+            if (lane_id == __ffsll((long long)want) - 1) {
+                if (J.xq) {
+                    const int lo = xq_lo(J, xr);
+                    s_base = lo + atomicAdd(J.xq + 32 * xr, nwant);
+                    s_lim = xr == 7 ? J.njobs : xq_lo(J, xr + 1);
+                } else {
+                    s_base = atomicAdd(J.counter, nwant);
+                    s_lim = J.njobs;
+                }
+            }
+            wave_jobs += (unsigned int)nwant;
             __builtin_amdgcn_wave_barrier();
             __syncthreads();
-            const int base = s_base;
+            const int base = s_base, lim = s_lim;
+            if (J.xq && base + nwant >= lim) {  // this group's range is used up: go on to the next
+                xr = (xr + 1) & 7;
+                ++xtried;
+            }
             if (idle) {
                 const int job_k = base + __popcll(want & ((1ull << lane_id) - 1ull));
-                if (job_k < J.njobs) {
+                if (job_k < lim) {
                     const int job = P.job_order ? P.job_order[job_k] : job_k;  // longest-first order
                     L.job = job;
                     L.sample = 0;
@@ -1606,7 +1644,7 @@ __global__ __launch_bounds__(64, WPE) void persistent_df_kernel(KParams P, JobSr
                         start = true;
                     }
                 } else {
-                    L.job = -2;  // no more work for this lane
+                    L.job = (J.xq && xtried < 8) ? -1 : -2;  // -2: no more work for this lane
                 }
             }
             __syncthreads();

@@ -70,6 +70,44 @@ struct rt_ctx {
     int wave_trace_n = 0;
 };
 
+// Image::Image + initMipmap (src/image.cpp:37-73,408-452): texel k = rgb[k*channels + 0..2] / 255.0f
+// (the reference strides by the file's channel count over the 3-channel stb buffer; bytes past
+// its end read as 0 here), then for square power-of-two images the chain down to 1x1, each texel
+// 0.25f * (((upper-left + lower-left) + upper-right) + lower-right).  Appends every level to
+// `out` (3 floats per texel); `levels` = mip levels including level 0, or 0 without a chain.
+static void build_texels(const rt_texture& t, std::vector<float>& out, int& levels) {
+    const size_t n = (size_t)t.width * t.height, nbytes = n * 3;
+    const size_t base = out.size();
+    out.resize(base + n * 3);
+    for (size_t k = 0; k < n; ++k)
+        for (int ch = 0; ch < 3; ++ch) {
+            const size_t i = k * (size_t)t.channels + ch;
+            out[base + 3 * k + ch] = (i < nbytes ? (float)t.rgb[i] : 0.0f) / 255.0f;
+        }
+    const int w = t.width, h = t.height;
+    const bool mip = ((h & (h - 1)) == 0) && ((w & (w - 1)) == 0) && (w == h);
+    levels = 0;
+    if (!mip) return;
+    levels = 1;
+    size_t prev = base;
+    for (int k = w; k > 1; k /= 2) {
+        const int rw = k / 2;
+        const size_t cur = out.size();
+        out.resize(cur + (size_t)rw * rw * 3);
+        for (int x = 0, rx = 0; x + 1 < k && rx < rw; x += 2, rx++)
+            for (int y = 0, ry = 0; y + 1 < k && ry < rw; y += 2, ry++)
+                for (int ch = 0; ch < 3; ++ch) {
+                    const float lu = out[prev + 3 * ((size_t)y * k + x) + ch];
+                    const float ll = out[prev + 3 * ((size_t)(y + 1) * k + x) + ch];
+                    const float ru = out[prev + 3 * ((size_t)y * k + x + 1) + ch];
+                    const float rl = out[prev + 3 * ((size_t)(y + 1) * k + x + 1) + ch];
+                    out[cur + 3 * ((size_t)ry * rw + rx) + ch] = 0.25f * (((lu + ll) + ru) + rl);
+                }
+        prev = cur;
+        ++levels;
+    }
+}
+
 // waves per SIMD the persistent kernel is compiled for (register cap); RT_WPE overrides for A/B runs
 static int wpe() {
     const char* w = std::getenv("RT_WPE");
@@ -121,12 +159,16 @@ static void launch_wide(int grid, hipStream_t st, const KParams& K, const JobSrc
             hipLaunchKernelGGL((persistent_df_kernel<COUNT, 4, BW>), dim3(grid), dim3(64), 0, st, K, J);
         else if (wpe() == 3)
             hipLaunchKernelGGL((persistent_df_kernel<COUNT, 3, BW>), dim3(grid), dim3(64), 0, st, K, J);
+        else if (!COUNT && !K.S.tex_on)  // production variant: no texture code at all
+            hipLaunchKernelGGL((persistent_df_kernel<false, 2, BW, false>), dim3(grid), dim3(64), 0, st, K, J);
         else
             hipLaunchKernelGGL((persistent_df_kernel<COUNT, 2, BW>), dim3(grid), dim3(64), 0, st, K, J);
         return;
     }
     if (wpe() == 1)
         hipLaunchKernelGGL((persistent_kernel<COUNT, 1, BW>), dim3(grid), dim3(64), 0, st, K, J);
+    else if (!COUNT && !K.S.tex_on && BW == 8)
+        hipLaunchKernelGGL((persistent_kernel<false, 2, 8, false>), dim3(grid), dim3(64), 0, st, K, J);
     else
         hipLaunchKernelGGL((persistent_kernel<COUNT, 2, BW>), dim3(grid), dim3(64), 0, st, K, J);
 }
@@ -169,6 +211,15 @@ static int persistent_grid(rt_ctx* c) {
     if (e != hipSuccess || per_cu <= 0) per_cu = 8;
     c->persistent_blocks[wpe()] = std::max(1, cus) * per_cu;
     return c->persistent_blocks[wpe()];
+}
+
+// d_stats: 16 counters, then the 8 per-XCD job heads (128-B apart) of the dynamic-fetch kernel
+#define RT_STATS_BYTES ((16 + 8 * 16) * sizeof(unsigned long long))
+
+// per-XCD job ranges for the dynamic-fetch kernel (RT_XCD=0: one global job counter)
+static bool use_xcd_queues() {
+    const char* x = std::getenv("RT_XCD");
+    return !(x && x[0] == '0');
 }
 
 static bool use_tile_kernel() {
@@ -414,6 +465,34 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
         spots[i].cos_angle = std::cos(L.angle * static_cast<float>(0.01745329251994329576923690768489));
     }
 
+    // kd textures: texels and mip chains (built here, once), per-mesh texture index
+    std::vector<float> texels;
+    std::vector<int4> tex_info;
+    std::vector<int> mat_tex(desc->num_meshes, -1);
+    for (int t = 0; t < desc->num_textures; ++t) {
+        const rt_texture& tx = desc->textures[t];
+        if (tx.width <= 0 || tx.height <= 0 || !tx.rgb || tx.channels < 3) {
+            set_error("rt_create: texture " + std::to_string(t) + " is invalid (needs >= 3 channels)");
+            rt_destroy(c);
+            return RT_ERR_INVALID;
+        }
+        int levels = 0;
+        const size_t off = texels.size() / 3;
+        build_texels(tx, texels, levels);
+        tex_info.push_back(make_int4((int)off, tx.width, tx.height, levels));
+    }
+    for (int m = 0; m < desc->num_meshes; ++m) {
+        const rt_material& sm = desc->materials[m];
+        if (!sm.has_texture) continue;
+        if (sm.texture >= 0 && sm.texture < desc->num_textures) mat_tex[m] = sm.texture;
+        else if (desc->num_textures > 0) {
+            set_error("rt_create: material " + std::to_string(m) + " names texture " + std::to_string(sm.texture) +
+                      " of " + std::to_string(desc->num_textures));
+            rt_destroy(c);
+            return RT_ERR_INVALID;
+        }
+    }
+
     DevScene& S = c->S;
     const float4* d_rec = nullptr;
     const float4* d_nodes = nullptr;
@@ -438,6 +517,10 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
     UP(desc->spherical_lights, (size_t)desc->num_spherical_lights, S.sl);
     UP(spots.data(), spots.size(), S.spot);
     UP(desc->plane_lights, (size_t)desc->num_plane_lights, S.plane);
+    UP(texels.data(), texels.size(), S.tex);
+    UP(tex_info.data(), tex_info.size(), S.tex_info);
+    UP(mat_tex.data(), mat_tex.size(), S.mat_tex);
+    S.ntex = desc->num_textures;
     S.ntri = ntri;
     S.nsph = desc->num_spheres;
     S.nref = (int)refn.size();
@@ -456,7 +539,7 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
     c->S8.tri = d_rec8;
     c->S8.nodes = d_nodes8;
 
-    if (hipMalloc(&c->d_stats, 16 * sizeof(unsigned long long)) != hipSuccess ||
+    if (hipMalloc(&c->d_stats, RT_STATS_BYTES) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
         set_error("rt_create: HIP allocation failed");
@@ -488,7 +571,21 @@ static int fill_params(rt_ctx* c, const rt_camera* cam, const rt_params* p, int 
         set_error("sample_size must be 4, 16 or 64");
         return RT_ERR_INVALID;
     }
+    if (p->texture_filtering < RT_TEX_NEAREST || p->texture_filtering > RT_TEX_TRILINEAR ||
+        p->out_of_bounds_x < RT_OOB_BORDER || p->out_of_bounds_x > RT_OOB_REPEAT ||
+        p->out_of_bounds_y < RT_OOB_BORDER || p->out_of_bounds_y > RT_OOB_REPEAT) {
+        set_error("texture_filtering / out_of_bounds rule out of range");
+        return RT_ERR_INVALID;
+    }
     std::memset(&K, 0, sizeof(K));
+    // per-render texture state (useTextures, textureFiltering, out-of-bounds rules, border colour)
+    for (DevScene* sc : {&c->S, &c->S8}) {
+        sc->tex_on = (p->use_textures && c->S.ntex > 0) ? 1 : 0;
+        sc->tex_filter = p->texture_filtering;
+        sc->tex_oob_x = p->out_of_bounds_x;
+        sc->tex_oob_y = p->out_of_bounds_y;
+        for (int k = 0; k < 3; ++k) sc->tex_border[k] = p->border_color[k];
+    }
     K.S = c->S;
     K.max_level = p->max_reflection_level;
     K.glossy_n = p->glossy_ray_count;
@@ -630,7 +727,7 @@ static int launch_wavefront(rt_ctx* c, const KParams& K0, const JobSrc& J, hipSt
     const int nchunks = (njobs + 63) / 64;
     const int seg = ((nchunks + WF_NQ - 1) / WF_NQ) * 64;
     const int cap = seg * WF_NQ;
-    const int fpj = std::max(1, K.max_level);
+    const int fpj = K.max_level + 1;  // frames 0..max_level (the deepest keeps its shading kd)
     int rc = ensure(c, &c->d_wf_st, &c->wf_st_bytes, (size_t)2 * WF_NFIELDS * cap * sizeof(float));
     if (rc != RT_OK) return rc;
     rc = ensure(c, &c->d_wf_res, &c->wf_res_bytes, (size_t)2 * cap * sizeof(float));
@@ -850,7 +947,7 @@ static int launch_render(rt_ctx* c, KParams& K, hipStream_t st, int count_mode, 
     const long long blocks = (long long)tiles_x * tiles_y * K.n_local_bands;
     float trace_ms = 0.0f;
     int trace_launches = 0;
-    HIP_TRY(hipMemsetAsync(c->d_stats, 0, 16 * sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(c->d_stats, 0, RT_STATS_BYTES, st));
     if (blocks > 0) {
         HIP_TRY(hipEventRecord(c->ev0, st));
         if (use_wavefront() && c->bw > 2) {
@@ -870,6 +967,7 @@ static int launch_render(rt_ctx* c, KParams& K, hipStream_t st, int count_mode, 
             J.mode = 0;
             J.njobs = (int)(blocks * 64);
             J.counter = reinterpret_cast<int*>(c->d_stats + 7);
+            J.xq = use_xcd_queues() ? reinterpret_cast<int*>(c->d_stats + 16) : nullptr;
             if (use_packets(c, K)) {
                 const int rc = launch_packets(c, K, st, count_mode, J.njobs);
                 if (rc != RT_OK) return rc;
@@ -1040,7 +1138,7 @@ extern "C" int rt_shade(rt_ctx* c, const rt_ray* rays, int n, const rt_params* p
         J.rays = d_r;
         J.rgb = d_c;
         J.ray_counts = d_n;
-        hipMemsetAsync(c->d_stats, 0, 16 * sizeof(unsigned long long), c->stream);
+        hipMemsetAsync(c->d_stats, 0, RT_STATS_BYTES, c->stream);
         const int rc = launch_wavefront(c, K, J, c->stream, 0, nullptr, nullptr);
         if (rc != RT_OK) {
             hipFree(d_r);
@@ -1058,7 +1156,8 @@ extern "C" int rt_shade(rt_ctx* c, const rt_ray* rays, int n, const rt_params* p
         J.rgb = d_c;
         J.ray_counts = d_n;
         J.counter = reinterpret_cast<int*>(c->d_stats + 7);
-        hipMemsetAsync(c->d_stats, 0, 16 * sizeof(unsigned long long), c->stream);
+        J.xq = use_xcd_queues() ? reinterpret_cast<int*>(c->d_stats + 16) : nullptr;
+        hipMemsetAsync(c->d_stats, 0, RT_STATS_BYTES, c->stream);
         const int grid = std::min((n + 63) / 64, persistent_grid(c));
         launch_persistent<false>(grid, c->stream, K, J, c);
     }

@@ -1,6 +1,8 @@
 // scene.cpp -- loadScene presets (reference src/scene.cpp:4-150), the flat scene-order view
 // (BoundingVolumeHierarchy::loadObjectsFromScene, src/bounding_volume_hierarchy.cpp:80-99) and the
 // deterministic dragon stand-in (data/dragon.obj is absent: .MISSING_LARGE_BLOBS:1).
+#include <iterator>
+#include <fstream>
 #include <cmath>
 #include <cstdio>
 #include <stdexcept>
@@ -46,7 +48,43 @@ void HostScene::flatten() {
         rm.shininess = m.material.shininess;
         rm.transparency = m.material.transparency;
         rm.has_texture = m.material.has_texture ? 1 : 0;
+        rm.texture = m.material.texture;
         flat_mat.push_back(rm);
+    }
+    flat_tex.clear();
+    for (const HostTexture& t : textures) {
+        rt_texture rt{};
+        rt.width = t.width;
+        rt.height = t.height;
+        rt.channels = t.channels;
+        rt.rgb = t.rgb.data();
+        flat_tex.push_back(rt);
+    }
+}
+
+void HostScene::load_textures() {
+    for (Mesh& m : meshes) {
+        Material& mat = m.material;
+        if (!mat.has_texture || mat.texture >= 0 || mat.texture_path.empty()) continue;
+        for (size_t i = 0; i < textures.size(); ++i)
+            if (textures[i].path == mat.texture_path) mat.texture = (int)i;
+        if (mat.texture >= 0) continue;
+        std::ifstream f(mat.texture_path, std::ios::binary);
+        if (!f) throw std::runtime_error("Texture file " + mat.texture_path + " does not exists!");
+        std::vector<uint8_t> bytes((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+        HostTexture t;
+        t.path = mat.texture_path;
+        if (rt_decode_png(bytes.data(), (long)bytes.size(), &t.width, &t.height, &t.channels, nullptr, 0) != RT_OK)
+            throw std::runtime_error("Failed to read texture " + mat.texture_path + " (PNG only)");
+        if (t.channels < 3)
+            throw std::runtime_error("Only textures with 3 or more color channels are supported. " + mat.texture_path +
+                                     " has " + std::to_string(t.channels) + " channels");
+        t.rgb.resize((size_t)t.width * t.height * 3);
+        if (rt_decode_png(bytes.data(), (long)bytes.size(), &t.width, &t.height, &t.channels, t.rgb.data(),
+                          (long)t.rgb.size()) != RT_OK)
+            throw std::runtime_error("Failed to read texture " + mat.texture_path);
+        mat.texture = (int)textures.size();
+        textures.push_back(std::move(t));
     }
 }
 
@@ -68,6 +106,8 @@ void HostScene::fill_desc(rt_scene_desc* d) const {
     d->spot_lights = spot_lights.empty() ? nullptr : spot_lights.data();
     d->num_plane_lights = (int)plane_lights.size();
     d->plane_lights = plane_lights.empty() ? nullptr : plane_lights.data();
+    d->num_textures = (int)flat_tex.size();
+    d->textures = flat_tex.empty() ? nullptr : flat_tex.data();
 }
 
 static void add_meshes(HostScene& s, std::vector<Mesh>&& sub) {

@@ -23,7 +23,13 @@ FLT_MAX = float(np.finfo(np.float32).max)
 
 class rt_material(C.Structure):
     _fields_ = [("kd", C.c_float * 3), ("ks", C.c_float * 3), ("shininess", C.c_float),
-                ("transparency", C.c_float), ("has_texture", C.c_int), ("pad_", C.c_int)]
+                ("transparency", C.c_float), ("has_texture", C.c_int), ("texture", C.c_int)]
+
+
+class rt_texture(C.Structure):
+    """Decoded kd texture (stbi_load(..., STBI_rgb) output, src/image.cpp:45)."""
+    _fields_ = [("width", C.c_int), ("height", C.c_int), ("channels", C.c_int), ("pad_", C.c_int),
+                ("rgb", C.POINTER(C.c_uint8))]
 
 
 class rt_sphere(C.Structure):
@@ -57,7 +63,8 @@ class rt_scene_desc(C.Structure):
                 ("point_lights", C.POINTER(rt_point_light)), ("num_spherical_lights", C.c_int),
                 ("spherical_lights", C.POINTER(rt_spherical_light)), ("num_spot_lights", C.c_int),
                 ("spot_lights", C.POINTER(rt_spot_light)), ("num_plane_lights", C.c_int),
-                ("plane_lights", C.POINTER(rt_plane_light))]
+                ("plane_lights", C.POINTER(rt_plane_light)), ("num_textures", C.c_int),
+                ("textures", C.POINTER(rt_texture))]
 
 
 class rt_camera(C.Structure):
@@ -70,7 +77,14 @@ class rt_params(C.Structure):
                 ("plane_light_1D_ray_count", C.c_int), ("glossy_ray_count", C.c_int),
                 ("refraction_factor", C.c_float), ("use_bvh", C.c_int), ("anti_aliasing", C.c_int),
                 ("multiple_rays", C.c_int), ("sample_size", C.c_int), ("barycentric_mode", C.c_int),
-                ("rng_seed", C.c_uint64)]
+                ("rng_seed", C.c_uint64), ("use_textures", C.c_int), ("texture_filtering", C.c_int),
+                ("out_of_bounds_x", C.c_int), ("out_of_bounds_y", C.c_int), ("border_color", C.c_float * 3),
+                ("pad_", C.c_int)]
+
+
+# TextureFiltering / OutOfBoundsRule (src/image.h:16-29)
+TEX_NEAREST, TEX_BILINEAR, TEX_MIP_NEAREST, TEX_MIP_NEAREST_BILINEAR, TEX_TRILINEAR = range(5)
+OOB_BORDER, OOB_CLAMP, OOB_REPEAT = range(3)
 
 
 class rt_ray(C.Structure):
@@ -103,7 +117,7 @@ EXPORTS = [
     "rt_destroy", "rt_render", "rt_render_device", "rt_unpermute_bands_device", "rt_intersect", "rt_shade",
     "rt_set_counting", "rt_debug_counters", "rt_ctx_info", "rt_selftest_math",
     "rt_postprocess_device", "rt_bitmap_device", "rt_postprocess", "rt_bitmap", "rt_encode_bmp", "rt_write_bmp",
-    "rt_philox4x32_10", "rt_debug_wave_trace",
+    "rt_philox4x32_10", "rt_debug_wave_trace", "rt_decode_png",
 ]
 
 class rt_post_params(C.Structure):
@@ -201,6 +215,8 @@ def lib():
             "rt_encode_bmp": ([C.c_int, C.c_int, P(C.c_uint8), P(C.c_uint8), C.c_long], C.c_long),
             "rt_write_bmp": ([C.c_char_p, C.c_int, C.c_int, P(C.c_uint8)], C.c_int),
             "rt_philox4x32_10": ([P(C.c_uint32), P(C.c_uint32), P(C.c_uint32)], C.c_int),
+            "rt_decode_png": ([P(C.c_uint8), C.c_long, P(C.c_int), P(C.c_int), P(C.c_int), P(C.c_uint8), C.c_long],
+                              C.c_int),
             "rt_debug_wave_trace": ([vp, P(C.c_uint64), C.c_int], C.c_int),
         }
         for name, (args, res) in sigs.items():
@@ -327,11 +343,25 @@ def aspect_of(W, H):
 
 
 def params(max_reflection_level=5, sphere_light_ray_count=10, plane_light_1D_ray_count=3, glossy_ray_count=10,
-           refraction_factor=0.8, use_bvh=False, anti_aliasing=False, multiple_rays=False, sample_size=4, seed=0x5EED):
+           refraction_factor=0.8, use_bvh=False, anti_aliasing=False, multiple_rays=False, sample_size=4, seed=0x5EED,
+           use_textures=False, texture_filtering=TEX_NEAREST, out_of_bounds_x=OOB_BORDER, out_of_bounds_y=OOB_BORDER,
+           border_color=(0.0, 0.0, 0.0)):
     """Render knobs with the reference defaults (src/main.cpp:54-64,123-127)."""
     return rt_params(max_reflection_level, sphere_light_ray_count, plane_light_1D_ray_count, glossy_ray_count,
                      float(np.float32(refraction_factor)), int(use_bvh), int(anti_aliasing), int(multiple_rays),
-                     sample_size, 0, seed)
+                     sample_size, 0, seed, int(use_textures), int(texture_filtering), int(out_of_bounds_x),
+                     int(out_of_bounds_y), _f3(border_color), 0)
+
+
+def decode_png(data):
+    """PNG bytes -> (H x W x 3 uint8 array, file channel count), stbi_load(..., STBI_rgb) semantics."""
+    buf = (C.c_uint8 * len(data)).from_buffer_copy(data)
+    w, h, n = C.c_int(), C.c_int(), C.c_int()
+    check(lib().rt_decode_png(buf, len(data), C.byref(w), C.byref(h), C.byref(n), None, 0), "rt_decode_png")
+    out = np.zeros((h.value, w.value, 3), np.uint8)
+    check(lib().rt_decode_png(buf, len(data), C.byref(w), C.byref(h), C.byref(n),
+                              out.ctypes.data_as(C.POINTER(C.c_uint8)), out.size), "rt_decode_png")
+    return out, n.value
 
 
 class Context:

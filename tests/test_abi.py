@@ -31,11 +31,12 @@ def test_library_exports_every_symbol(R):
 
 
 def test_abi_version_and_struct_sizes(R):
-    assert R.lib().rt_abi_version() == 1
+    assert R.lib().rt_abi_version() == 2
     assert ctypes.sizeof(R.rt_material) == 40
     assert ctypes.sizeof(R.rt_ray) == 28
     assert ctypes.sizeof(R.rt_hit) == 52
-    assert ctypes.sizeof(R.rt_params) == 48
+    assert ctypes.sizeof(R.rt_params) == 80
+    assert ctypes.sizeof(R.rt_texture) == 24
 
 
 def test_no_cpu_fallback_without_gpu(R):
