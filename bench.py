@@ -44,9 +44,13 @@ def kernel_name(ntri):
     bw = bw if bw in ("2", "4") else "8"
     if k == "wavefront":
         return f"rt::wf_trace_kernel<false, 4, {bw}>"
+    # wpe 2 without textures launches the TEX=false specialisation (no texture code); the
+    # persistent kernel has it for the 8-wide BVH only
     if k == "persistent" or (k != "df" and ntri < 65536) or bw == "2":
-        return f"rt::persistent_kernel<false, {wpe}, {bw}>"
-    return f"rt::persistent_df_kernel<false, {wpe}, {bw}>"
+        tex = ", false" if (wpe == 2 and bw == "8") else ""
+        return f"rt::persistent_kernel<false, {wpe}, {bw}{tex}>"
+    tex = ", false" if wpe == 2 else ""
+    return f"rt::persistent_df_kernel<false, {wpe}, {bw}{tex}>"
 
 
 def cpu_baseline(config, budget_s=12.0, seed=12345):

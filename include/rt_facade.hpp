@@ -130,6 +130,16 @@ inline Scene loadScene(SceneType type, const std::string& dataDir) {
     return s;
 }
 
+// TextureFiltering / OutOfBoundsRule (src/image.h:16-29)
+enum class TextureFiltering {
+    NearestNeighbor = RT_TEX_NEAREST,
+    Bilinear = RT_TEX_BILINEAR,
+    MipMappingNearestLevelNearestNeighbor = RT_TEX_MIP_NEAREST,
+    MipMappingNearestLevelBilinear = RT_TEX_MIP_NEAREST_BILINEAR,
+    Trilinear = RT_TEX_TRILINEAR
+};
+enum class OutOfBoundsRule { Border = RT_OOB_BORDER, Clamp = RT_OOB_CLAMP, Repeat = RT_OOB_REPEAT };
+
 // Render knobs = the reference's globals (src/main.cpp:54-64,123-127)
 struct RenderSettings {
     int max_reflection_level = 5;
@@ -138,6 +148,11 @@ struct RenderSettings {
     int glossy_ray_count = 1;  // reference default 10 draws rand(); 1 is deterministic
     float refraction_factor = 0.8f;
     bool useBVH = false;
+    bool useTextures = false;
+    TextureFiltering textureFiltering = TextureFiltering::NearestNeighbor;
+    OutOfBoundsRule outOfBoundsRuleX = OutOfBoundsRule::Border;
+    OutOfBoundsRule outOfBoundsRuleY = OutOfBoundsRule::Border;
+    vec3 textureBorderColor{0.0f, 0.0f, 0.0f};
     rt_params to_c() const {
         rt_params p{};
         p.max_reflection_level = max_reflection_level;
@@ -147,6 +162,13 @@ struct RenderSettings {
         p.refraction_factor = refraction_factor;
         p.use_bvh = useBVH ? 1 : 0;
         p.sample_size = 4;
+        p.use_textures = useTextures ? 1 : 0;
+        p.texture_filtering = (int)textureFiltering;
+        p.out_of_bounds_x = (int)outOfBoundsRuleX;
+        p.out_of_bounds_y = (int)outOfBoundsRuleY;
+        p.border_color[0] = textureBorderColor.x;
+        p.border_color[1] = textureBorderColor.y;
+        p.border_color[2] = textureBorderColor.z;
         return p;
     }
 };
