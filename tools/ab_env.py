@@ -27,8 +27,10 @@ for cfg in cfgs:
     cam = R.camera_from_trackball(aspect=R.aspect_of(W, H))
     res = {n: [] for n, _ in variants}
     ref = None
-    for _ in range(rounds):
-        for n, env in variants:
+    ctx.render(cam, p, W, H)  # warm-up (code object load, scratch)
+    for rd in range(rounds):
+        order = variants[rd % len(variants):] + variants[:rd % len(variants)]  # rotate: no first-slot bias
+        for n, env in order:
             for k in keys:
                 os.environ.pop(k, None)
             os.environ.update(env)
