@@ -114,6 +114,10 @@ def main():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--partition", choices=("frames", "bands"), default="frames",
+                    help="N>1: frames = every rank renders whole frames of its own (weak scaling, no collective "
+                         "on the data path); bands = one frame split into interleaved 8-row bands, RCCL "
+                         "all-gather, un-permute on rank 0 (strong scaling, single-frame latency)")
     args = ap.parse_args()
 
     import torch
@@ -134,19 +138,22 @@ def main():
     ctx = R.Context(scene, device=local)
     upload_s = time.perf_counter() - t_up
 
+    # frames: each rank is a band split of one (count = 1) -- a whole frame, un-permuted locally
+    bands = args.partition == "bands" and world > 1
+    b_rank, b_count = (rank, world) if bands else (0, 1)
     nbands = (H + BAND_ROWS - 1) // BAND_ROWS
-    max_local = (nbands + world - 1) // world
+    max_local = (nbands + b_count - 1) // b_count
     local_buf = torch.zeros(max_local * BAND_ROWS * W * 3, dtype=torch.float32, device=dev)
-    gathered = torch.zeros(world * local_buf.numel(), dtype=torch.float32, device=dev) if world > 1 else local_buf
+    gathered = torch.zeros(world * local_buf.numel(), dtype=torch.float32, device=dev) if bands else local_buf
     image = torch.zeros(W * H * 3, dtype=torch.float32, device=dev)
 
     def step():
         stream = torch.cuda.current_stream(dev).cuda_stream
-        st = ctx.render_device(cam, prm, W, H, BAND_ROWS, rank, world, local_buf.data_ptr(), stream)
-        if world > 1:
+        st = ctx.render_device(cam, prm, W, H, BAND_ROWS, b_rank, b_count, local_buf.data_ptr(), stream)
+        if bands:
             dist.all_gather_into_tensor(gathered, local_buf)
-        if rank == 0:
-            R.check(R.lib().rt_unpermute_bands_device(W, H, BAND_ROWS, world, R.C.c_void_p(gathered.data_ptr()),
+        if rank == 0 or not bands:
+            R.check(R.lib().rt_unpermute_bands_device(W, H, BAND_ROWS, b_count, R.C.c_void_p(gathered.data_ptr()),
                                                       R.C.c_void_p(image.data_ptr()), R.C.c_void_p(stream)))
         return st
 
@@ -186,7 +193,7 @@ def main():
 
     if rank == 0:
         # roofline of the dominant kernel (render_kernel) on rank 0's launches
-        pixels0 = int(((nbands - rank + world - 1) // world) * BAND_ROWS * W)
+        pixels0 = int(((nbands - b_rank + b_count - 1) // b_count) * BAND_ROWS * W)
         bytes0 = algorithmic_bytes(cst, min(pixels0, W * H))
         avg_ms = float(np.mean(kms))
         achieved = bytes0 / (avg_ms * 1e-3) / 1e9
@@ -201,12 +208,14 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": max_elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "strong" if bands else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (deterministic 800k-triangle torus-knot stand-in for the missing data/dragon.obj)",
             "config": {"workload": f"{args.config}: {desc}", "resolution": f"{W}x{H}", "rays_per_frame":
-                       int(total_rays / args.steps), "band_rows": BAND_ROWS, "partition": f"{world} GPU band split",
+                       int(total_rays / args.steps / (1 if bands else world)), "band_rows": BAND_ROWS,
+                       "partition": (f"one frame, {world}-GPU band split" if bands else
+                                     f"{world} GPU(s), a whole frame per GPU per step"),
                        "scene_upload_s": round(upload_s, 3)},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,

@@ -138,6 +138,7 @@ struct Cnt {
     uint32_t rays, nodes, tris, hits;
     uint32_t wnodes, wtris, wadv;  // wave-level steps (counted by the first active lane): SIMD efficiency
     unsigned long long cyc_a, cyc_b;  // shader clocks per wave in the state machine / in traversal (df kernel)
+    unsigned long long cyc_c, cyc_d;  // ... of cyc_a: advancing finished queries / fetching jobs
 };
 
 // true on the lowest active lane of the wave (counting builds: one count per wave instruction stream)
@@ -895,6 +896,8 @@ __device__ void flush_counters(const KParams& P, const Cnt& c) {
             atomicAdd(P.stats + 6, wa);
             atomicAdd(P.stats + 8, c.cyc_a);
             atomicAdd(P.stats + 9, c.cyc_b);
+            atomicAdd(P.stats + 10, c.cyc_c);
+            atomicAdd(P.stats + 11, c.cyc_d);
         }
     }
 }
