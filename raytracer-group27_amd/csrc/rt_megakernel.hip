@@ -1582,6 +1582,8 @@ __global__ __launch_bounds__(64, WPE) void persistent_df_kernel(KParams P, JobSr
             if (COUNT && wave_leader()) cnt.wadv++;
             start = advance_lane<COUNT, TEX>(P, J, L, fr, T.found, T.best, cnt, job_cnt);
         }
+        const unsigned long long tJ = COUNT ? (unsigned long long)clock64() : 0ull;
+        if (COUNT) cnt.cyc_c += tJ - tA;  // state machine
         const bool idle = (L.job == -1);
         const unsigned long long want = __ballot(idle);
         if (want) {
@@ -1649,6 +1651,7 @@ __global__ __launch_bounds__(64, WPE) void persistent_df_kernel(KParams P, JobSr
             }
             __syncthreads();
         }
+        if (COUNT) cnt.cyc_d += (unsigned long long)clock64() - tJ;  // job fetch and camera rays
         if (start) {
             cnt.rays++;
             job_cnt.rays++;
