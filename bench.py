@@ -2,11 +2,15 @@
 
 Workload (config.workload): C3 = dragon proxy (800 000 triangles), 1920x1080,
 one point light, hard shadows + mirror recursion depth 4 (BASELINE.json configs[2]).  One step
-renders one full frame: every rank renders its interleaved 8-row bands on its own GPU, the bands
-are gathered over RCCL (torch.distributed "nccl") and rank 0 un-permutes them into the
-Screen::m_textureData layout.  Inputs (scene, BVH) are resident in HBM before timing starts.
+renders a batch of --views full frames (default 8: a turntable of the scene, 45 degrees apart) in
+ONE launch of the persistent kernel (rt_render_views_device), each frame un-permuted into its own
+Screen::m_textureData image; every rank renders its own batch (weak scaling, no collective on the
+data path).  --views 1 renders one frame per step; --partition bands splits one frame over the
+ranks in interleaved 8-row bands, gathered over RCCL (torch.distributed "nccl") and un-permuted
+on rank 0.  Inputs (scene, BVH) are resident in HBM before timing starts.  The JSON also carries
+`single_frame`: the default view rendered alone (one launch per frame), timed the same way.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3] [--views V] [--no-cpu-baseline]
 
 Prints ONE JSON line on rank 0.  `value` = rays (intersect() calls) of all ranks / max-rank time.
 """
@@ -24,6 +28,7 @@ import numpy as np  # noqa: E402
 METRIC = "Mrays/s (primary+shadow+secondary) at 1920×1080; fraction of HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 BAND_ROWS = 8
+DEFAULT_VIEWS = 8  # frames per step: an 8-view turntable (45 deg apart) of the C3 scene in one launch
 
 
 def algorithmic_bytes(st, pixels):
@@ -114,10 +119,18 @@ def main():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--no-single-frame", action="store_true",
+                    help="skip the single-frame latency record (profiling runs: one kernel shape only)")
     ap.add_argument("--partition", choices=("frames", "bands"), default="frames",
                     help="N>1: frames = every rank renders whole frames of its own (weak scaling, no collective "
                          "on the data path); bands = one frame split into interleaved 8-row bands, RCCL "
                          "all-gather, un-permute on rank 0 (strong scaling, single-frame latency)")
+    ap.add_argument("--views", type=int, default=None,
+                    help="frames per step (default 8; 1 with --partition bands): a turntable batch of this many "
+                         "views of the scene rendered in ONE launch (rt_render_views_device; the drain tail of one "
+                         "frame overlaps the next), every frame un-permuted into its own Screen-layout image")
+    ap.add_argument("--view-step", type=float, default=None,
+                    help="turntable step between views in degrees (default 360 / views)")
     args = ap.parse_args()
 
     import torch
@@ -133,7 +146,12 @@ def main():
     dev = torch.device("cuda", local)
 
     scene, prm, W, H, desc = R.build_config(args.config)
-    cam = R.camera_from_trackball(aspect=R.aspect_of(W, H))
+    if args.views is None:
+        args.views = 1 if (args.partition == "bands" and world > 1) else DEFAULT_VIEWS
+    F = max(1, args.views)
+    if F > 1 and args.partition == "bands" and world > 1:
+        sys.exit("--views > 1 renders whole frames per rank; use --partition frames")
+    cams = R.turntable_cameras(F, R.aspect_of(W, H), args.view_step) if F > 1 else [R.camera_from_trackball(aspect=R.aspect_of(W, H))]
     t_up = time.perf_counter()
     ctx = R.Context(scene, device=local)
     upload_s = time.perf_counter() - t_up
@@ -143,18 +161,31 @@ def main():
     b_rank, b_count = (rank, world) if bands else (0, 1)
     nbands = (H + BAND_ROWS - 1) // BAND_ROWS
     max_local = (nbands + b_count - 1) // b_count
-    local_buf = torch.zeros(max_local * BAND_ROWS * W * 3, dtype=torch.float32, device=dev)
+    view_elems = max_local * BAND_ROWS * W * 3
+    local_buf = torch.zeros(F * view_elems, dtype=torch.float32, device=dev)
     gathered = torch.zeros(world * local_buf.numel(), dtype=torch.float32, device=dev) if bands else local_buf
-    image = torch.zeros(W * H * 3, dtype=torch.float32, device=dev)
+    image = torch.zeros(F * W * H * 3, dtype=torch.float32, device=dev)
+
+    # one explicit stream for render, gather and un-permute (torch's default stream is the null
+    # stream, which would let the un-permute of step k overlap the render of step k+1)
+    bstream = torch.cuda.Stream(dev)
 
     def step():
-        stream = torch.cuda.current_stream(dev).cuda_stream
-        st = ctx.render_device(cam, prm, W, H, BAND_ROWS, b_rank, b_count, local_buf.data_ptr(), stream)
+        with torch.cuda.stream(bstream):
+            return _step(bstream.cuda_stream)
+
+    def _step(stream):
+        if F > 1:
+            st = ctx.render_views_device(cams, prm, W, H, BAND_ROWS, 0, 1, local_buf.data_ptr(), stream)
+        else:
+            st = ctx.render_device(cams[0], prm, W, H, BAND_ROWS, b_rank, b_count, local_buf.data_ptr(), stream)
         if bands:
             dist.all_gather_into_tensor(gathered, local_buf)
         if rank == 0 or not bands:
-            R.check(R.lib().rt_unpermute_bands_device(W, H, BAND_ROWS, b_count, R.C.c_void_p(gathered.data_ptr()),
-                                                      R.C.c_void_p(image.data_ptr()), R.C.c_void_p(stream)))
+            for v in range(F):
+                R.check(R.lib().rt_unpermute_bands_device(
+                    W, H, BAND_ROWS, b_count, R.C.c_void_p(gathered.data_ptr() + 4 * v * view_elems),
+                    R.C.c_void_p(image.data_ptr() + 4 * v * W * H * 3), R.C.c_void_p(stream)))
         return st
 
     # counting pass (same kernel, COUNT=true) for the algorithmic-byte roofline numerator
@@ -180,6 +211,23 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
 
+    # single-frame latency beside the batch: the default view alone, one launch per frame
+    single = None
+    if F > 1 and not args.no_single_frame:
+        one = ctx.render_device(cams[0], prm, W, H, BAND_ROWS, 0, 1, local_buf.data_ptr(), None)
+        n1 = max(5, args.steps)
+        barrier()
+        t1 = time.perf_counter()
+        r1, k1 = 0, []
+        for _ in range(n1):
+            one = ctx.render_device(cams[0], prm, W, H, BAND_ROWS, 0, 1, local_buf.data_ptr(), None)
+            r1 += one.rays
+            k1.append(one.kernel_ms)
+        barrier()
+        e1 = time.perf_counter() - t1
+        single = {"ms_per_frame": e1 / n1 * 1e3, "kernel_ms": float(np.mean(k1)), "rays_per_frame": int(one.rays),
+                  "Mrays_per_s_per_gpu": r1 / e1 / 1e6, "frames": n1}
+
     t = torch.tensor([elapsed, float(rays), float(np.mean(kms)), float(cst.node_visits), float(cst.tri_tests),
                       float(cst.hits), float(cst.rays)], dtype=torch.float64, device=dev)
     if world > 1:
@@ -194,11 +242,11 @@ def main():
     if rank == 0:
         # roofline of the dominant kernel (render_kernel) on rank 0's launches
         pixels0 = int(((nbands - b_rank + b_count - 1) // b_count) * BAND_ROWS * W)
-        bytes0 = algorithmic_bytes(cst, min(pixels0, W * H))
+        bytes0 = algorithmic_bytes(cst, F * min(pixels0, W * H))
         avg_ms = float(np.mean(kms))
         achieved = bytes0 / (avg_ms * 1e-3) / 1e9
         kname = kernel_name(ctx.info()["tri_records"])
-        pmc = load_pmc(args.config, kname)
+        pmc = load_pmc(args.config if F == 1 else f"{args.config}/v{F}", kname)
         line = {
             "metric": METRIC,
             "value": total_rays / max_elapsed / 1e6,
@@ -212,10 +260,13 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (deterministic 800k-triangle torus-knot stand-in for the missing data/dragon.obj)",
-            "config": {"workload": f"{args.config}: {desc}", "resolution": f"{W}x{H}", "rays_per_frame":
-                       int(total_rays / args.steps / (1 if bands else world)), "band_rows": BAND_ROWS,
+            "config": {"workload": f"{args.config}: {desc}" + (f"; {F} turntable views per step (one launch)"
+                                                                  if F > 1 else ""),
+                       "resolution": f"{W}x{H}", "frames_per_step": F, "ms_per_frame": max_elapsed / args.steps / F * 1e3,
+                       "rays_per_frame": int(total_rays / args.steps / (1 if bands else world) / F),
+                       "band_rows": BAND_ROWS,
                        "partition": (f"one frame, {world}-GPU band split" if bands else
-                                     f"{world} GPU(s), a whole frame per GPU per step"),
+                                     f"{world} GPU(s), {F} whole frame(s) per GPU per step"),
                        "scene_upload_s": round(upload_s, 3)},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
@@ -223,6 +274,8 @@ def main():
                          "kernel": kname, "kernel_avg_ms": avg_ms,
                          "algorithmic_bytes_per_launch": int(bytes0)},
         }
+        if single is not None:
+            line["single_frame"] = single
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.config, budget_s=args.cpu_budget)
         print(json.dumps(line), flush=True)

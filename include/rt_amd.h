@@ -13,6 +13,7 @@
  *   rt_render            static void renderRayTracing(Scene&, const Trackball&, const BVH&, Screen&, ...)
  *                        src/main.cpp:340-400 (+ Screen::setPixel src/screen.cpp:32-38)
  *   rt_render_device     same as rt_render, band-partitioned, device-resident output (multi-GPU path)
+ *   rt_render_views_device  a batch of rt_render_device frames (one camera each) in one launch
  *   rt_camera_from_trackball  Trackball::generateRay / position(), framework/src/trackball.cpp:65-98
  *   rt_scene_load_obj    std::vector<Mesh> loadMesh(path, bool normalize), src/mesh.cpp:58-188
  *   rt_scene_preset      Scene loadScene(SceneType, dataDir), src/scene.cpp:4-150
@@ -34,7 +35,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2  /* 2: textures (rt_texture, rt_params texture fields) */
+#define RT_ABI_VERSION 3  /* 2: textures (rt_texture, rt_params texture fields); 3: rt_render_views_device */
 
 /* status codes */
 #define RT_OK 0
@@ -220,6 +221,11 @@ int rt_camera_from_trackball(const float look_at[3], const float euler_radians[3
                              float fovy_radians, float aspect, rt_camera* out);
 
 /* ---- device context ---- */
+/* Number of visible HIP devices (initialises this library's HIP runtime); RT_ERR_NO_DEVICE (n = 0)
+ * without a GPU.  In a process that also hosts PyTorch's bundled copy of the HIP runtime, let
+ * torch initialise the GPU before this library is loaded (rt_amd.py does; the other order leaves
+ * one of the two runtimes without a device). */
+int rt_device_count(int* n);
 int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out);
 int rt_destroy(rt_ctx* ctx);
 
@@ -237,6 +243,19 @@ int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_params* params, int wi
 int rt_render_device(rt_ctx* ctx, const rt_camera* cam, const rt_params* params, int width,
                      int height, int band_rows, int band_rank, int band_count, float* d_rgb_out,
                      void* stream, rt_stats* stats);
+/*
+ * View batch: n_views frames of the same scene (one camera each, e.g. a turntable or a multi-view
+ * capture) in ONE launch -- a sequence of renderRayTracing calls (src/main.cpp:340-400), one per
+ * camera change of the trackball (framework/src/trackball.cpp:87-98).  The persistent job queue
+ * spans every view, so the drain tail of one frame overlaps the start of the next.  d_rgb_out
+ * holds n_views rt_render_device buffers back to back (view v at v * n_local_bands * band_rows *
+ * width * 3 floats); view v's buffer is bit-identical to rt_render_device with cams[v].  Stats
+ * are summed over the views.  Persistent kernels only (RT_KERNEL=tile/wavefront, RT_PACKET=1 and
+ * RT_SCHED are rejected with RT_ERR_INVALID).  n_views == 1 is rt_render_device.
+ */
+int rt_render_views_device(rt_ctx* ctx, const rt_camera* cams, int n_views, const rt_params* params,
+                           int width, int height, int band_rows, int band_rank, int band_count,
+                           float* d_rgb_out, void* stream, rt_stats* stats);
 /* Un-permute gathered band buffers ([band_count][max_local_bands][band_rows][W][3]) into the
  * setPixel layout on the device. */
 int rt_unpermute_bands_device(int width, int height, int band_rows, int band_count,

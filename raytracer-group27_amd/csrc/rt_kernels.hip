@@ -110,6 +110,10 @@ struct KParams {
     int coop;                        // dynamic-fetch kernel: lane-group traversal of the drain's queries
     int coop_max;                    // ... when at most this many queries are left in the wave
     int coop_reserve;                // ... free pool slots kept for depth-first steps
+    // view batch (rt_render_views_device): n_views frames of the same scene in one launch, view v's
+    // camera at views[12 v] (cam xyz, quat wxyz, hh, hw), its rows at out + v * view_rows * W * 3
+    int n_views, view_jobs, view_rows;
+    const float* views;
 };
 
 // Philox-4x32-10 (Salmon et al., SC'11; the Random123 constants): the counter-based stream that
@@ -863,6 +867,14 @@ __device__ __forceinline__ void gen_ray(const KParams& P, float px, float py, v3
     const v3 csd = normalize(v3{-px * P.hw, py * P.hh, 1.0f});
     o = v3{P.cam[0], P.cam[1], P.cam[2]};
     d = quat_rotate(P.q[0], P.q[1], P.q[2], P.q[3], csd);
+}
+
+// camera ray of view v of a view batch (the same Trackball::generateRay arithmetic, per-view camera)
+__device__ __forceinline__ void gen_ray_view(const KParams& P, int v, float px, float py, v3& o, v3& d) {
+    const float* c = P.views + 12 * v;
+    const v3 csd = normalize(v3{-px * c[8], py * c[7], 1.0f});
+    o = v3{c[0], c[1], c[2]};
+    d = quat_rotate(c[3], c[4], c[5], c[6], csd);
 }
 
 template <bool COUNT>

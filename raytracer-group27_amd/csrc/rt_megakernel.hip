@@ -720,11 +720,31 @@ struct JobSrc {
     int* counter;                  // global job counter (zeroed per launch)
     int* xq;  // dynamic-fetch kernel, or null: 8 job heads (32-int spacing, zeroed per launch), one
               // per group of blocks sharing an XCD (blockIdx % 8), each over 1/8 of the jobs
+    int n_views;    // view batch: njobs = n_views * view_jobs
+    int view_jobs;  // jobs of one view (a multiple of 64)
 };
 
 // Job range of XCD group x: a contiguous run of 8x8 tiles (a horizontal band of the frame), so
 // the rays of one XCD touch the geometry of one band and its L2 holds that part of the scene.
-__device__ __forceinline__ int xq_lo(const JobSrc& J, int x) { return ((x * ((J.njobs + 63) >> 6)) >> 3) << 6; }
+// A view batch keeps the split per view: range x holds band x of view 0, then band x of view 1, ...
+__device__ __forceinline__ int xq_lo(const JobSrc& J, int x) {
+    return J.n_views * (((x * ((J.view_jobs + 63) >> 6)) >> 3) << 6);
+}
+
+// Job index of a view batch -> (view, job inside the view): the inverse of the range layout above
+// (identity for one view).
+__device__ __forceinline__ int view_job(const KParams& P, int g, int& v) {
+    v = 0;
+    if (P.n_views <= 1) return g;
+    const int nt = (P.view_jobs + 63) >> 6;
+    int x = 7;
+    while (x > 0 && g < P.n_views * (((x * nt) >> 3) << 6)) --x;
+    const int lo = ((x * nt) >> 3) << 6;
+    const int hi = x == 7 ? P.view_jobs : (((x + 1) * nt) >> 3) << 6;
+    const int k = g - P.n_views * lo;
+    v = k / (hi - lo);
+    return lo + (k - v * (hi - lo));
+}
 
 // queue the camera ray of the lane's current sample (src/main.cpp:350-386)
 __device__ __forceinline__ void queue_camera(const KParams& P, Lane& L) {
@@ -748,7 +768,10 @@ __device__ __forceinline__ void queue_camera(const KParams& P, Lane& L) {
         sy = ndy + (P.ms_offy * qy * (float)yy);
     }
     v3 o, d;
-    gen_ray(P, sx, sy, o, d);
+    if (P.n_views > 1)
+        gen_ray_view(P, L.out_row / P.view_rows, sx, sy, o, d);
+    else
+        gen_ray(P, sx, sy, o, d);
     L.qo = o;
     L.qd = d;
     L.qt = FLT_MAX;
@@ -759,7 +782,9 @@ __device__ __forceinline__ void queue_camera(const KParams& P, Lane& L) {
 }
 
 // Map a job index to its pixel (8x8 tiles inside the rank's bands).  False if outside the image.
-__device__ __forceinline__ bool job_pixel(const KParams& P, int job, Lane& L) {
+__device__ __forceinline__ bool job_pixel(const KParams& P, int gjob, Lane& L) {
+    int view;
+    const int job = view_job(P, gjob, view);
     const int tiles_x = (P.W + 7) / 8;
     const int tiles_y_band = (P.band_rows + 7) / 8;
     const int tile = job >> 6;
@@ -772,7 +797,7 @@ __device__ __forceinline__ bool job_pixel(const KParams& P, int job, Lane& L) {
     const int row_in_band = ty * 8 + (lane >> 3);
     L.px = tx * 8 + (lane & 7);
     L.py = gb * P.band_rows + row_in_band;
-    L.out_row = lb * P.band_rows + row_in_band;
+    L.out_row = view * P.view_rows + lb * P.band_rows + row_in_band;
     return (L.px < P.W) && (row_in_band < P.band_rows) && (L.py < P.H) && (lb < P.n_local_bands);
 }
 

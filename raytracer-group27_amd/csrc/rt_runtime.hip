@@ -68,6 +68,9 @@ struct rt_ctx {
     float* d_wave_trace = nullptr;
     size_t wave_trace_bytes = 0;
     int wave_trace_n = 0;
+    // view batch (rt_render_views_device): per-view cameras, 12 floats each
+    float* d_views = nullptr;
+    size_t views_bytes = 0;
 };
 
 // Image::Image + initMipmap (src/image.cpp:37-73,408-452): texel k = rgb[k*channels + 0..2] / 255.0f
@@ -274,6 +277,7 @@ extern "C" int rt_destroy(rt_ctx* c) {
     if (c->d_wf_cnt) hipFree(c->d_wf_cnt);
     if (c->d_pre) hipFree(c->d_pre);
     if (c->d_wave_trace) hipFree(c->d_wave_trace);
+    if (c->d_views) hipFree(c->d_views);
     if (c->d_sched) hipFree(c->d_sched);
     if (c->d_cost) hipFree(c->d_cost);
     if (c->h_wf_cnt) hipHostFree(c->h_wf_cnt);
@@ -290,6 +294,22 @@ static float glossy_width(float shininess) {
     return (float)((double)std::pow(0.5f, -1 / shininess) * std::sqrt(1 - std::pow(0.5, (double)(2 / shininess))));
 }
 
+// Visible devices (initialises this library's HIP runtime).
+extern "C" int rt_device_count(int* n) {
+    if (!n) {
+        set_error("rt_device_count: null argument");
+        return RT_ERR_INVALID;
+    }
+    *n = 0;
+    const hipError_t e = hipGetDeviceCount(n);
+    if (e != hipSuccess) {
+        *n = 0;
+        set_error(std::string("rt_device_count: ") + hipGetErrorString(e));
+        return RT_ERR_NO_DEVICE;
+    }
+    return RT_OK;
+}
+
 extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
     if (!desc || !out) {
         set_error("rt_create: null argument");
@@ -297,8 +317,10 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
     }
     *out = nullptr;
     int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
-        set_error("rt_create: no HIP device available (the MI355X path has no CPU fallback)");
+    const hipError_t de = hipGetDeviceCount(&ndev);
+    if (de != hipSuccess || ndev == 0) {
+        set_error(std::string("rt_create: no HIP device available (the MI355X path has no CPU fallback): ") +
+                  (de != hipSuccess ? hipGetErrorString(de) : "0 devices"));
         return RT_ERR_NO_DEVICE;
     }
     if (device < 0 || device >= ndev) {
@@ -613,6 +635,7 @@ static int fill_params(rt_ctx* c, const rt_camera* cam, const rt_params* p, int 
     }
     K.W = W;
     K.H = H;
+    K.n_views = 1;
     K.aa = p->anti_aliasing ? 1 : 0;
     K.multi = (!p->anti_aliasing && p->multiple_rays) ? 1 : 0;
     K.sample_size = p->sample_size;
@@ -955,6 +978,8 @@ static int launch_render(rt_ctx* c, KParams& K, hipStream_t st, int count_mode, 
             JobSrc J{};
             J.mode = 0;
             J.njobs = (int)(blocks * 64);
+            J.n_views = 1;
+            J.view_jobs = J.njobs;
             int rc = launch_wavefront(c, K, J, st, count_mode, stats ? &trace_ms : nullptr,
                                       stats ? &trace_launches : nullptr);
             if (rc != RT_OK) return rc;
@@ -966,7 +991,10 @@ static int launch_render(rt_ctx* c, KParams& K, hipStream_t st, int count_mode, 
         } else {
             JobSrc J{};
             J.mode = 0;
-            J.njobs = (int)(blocks * 64);
+            J.n_views = std::max(1, K.n_views);
+            J.view_jobs = (int)(blocks * 64);
+            J.njobs = J.n_views * J.view_jobs;
+            K.view_jobs = J.view_jobs;
             J.counter = reinterpret_cast<int*>(c->d_stats + 7);
             J.xq = use_xcd_queues() ? reinterpret_cast<int*>(c->d_stats + 16) : nullptr;
             if (use_packets(c, K)) {
@@ -1040,6 +1068,53 @@ extern "C" int rt_render_device(rt_ctx* c, const rt_camera* cam, const rt_params
     K.n_local_bands = nbands > band_rank ? (nbands - band_rank + band_count - 1) / band_count : 0;
     K.out = d_out;
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    return launch_render(c, K, st, g_count_mode, stats);
+}
+
+extern "C" int rt_render_views_device(rt_ctx* c, const rt_camera* cams, int n_views, const rt_params* p, int W, int H,
+                                      int band_rows, int band_rank, int band_count, float* d_out, void* stream,
+                                      rt_stats* stats) {
+    if (!c || !cams || n_views <= 0 || !p || !d_out || W <= 0 || H <= 0 || band_rows <= 0 || band_count <= 0 ||
+        band_rank < 0 || band_rank >= band_count) {
+        set_error("rt_render_views_device: invalid argument");
+        return RT_ERR_INVALID;
+    }
+    if (n_views == 1)
+        return rt_render_device(c, cams, p, W, H, band_rows, band_rank, band_count, d_out, stream, stats);
+    if (use_wavefront() || use_tile_kernel() || (std::getenv("RT_PACKET") && std::getenv("RT_PACKET")[0] == '1') || std::getenv("RT_SCHED")) {
+        set_error("rt_render_views_device: view batches run on the persistent kernels only");
+        return RT_ERR_INVALID;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    KParams K;
+    int rc = fill_params(c, cams, p, W, H, K);
+    if (rc != RT_OK) return rc;
+    const int nbands = (H + band_rows - 1) / band_rows;
+    K.band_rows = band_rows;
+    K.band_rank = band_rank;
+    K.band_count = band_count;
+    K.n_local_bands = nbands > band_rank ? (nbands - band_rank + band_count - 1) / band_count : 0;
+    const long long view_jobs = (long long)((W + 7) / 8) * ((band_rows + 7) / 8) * K.n_local_bands * 64;
+    if (view_jobs * n_views > 0x7FFFFFFFll) {
+        set_error("rt_render_views_device: batch too large (job index overflows int)");
+        return RT_ERR_INVALID;
+    }
+    K.out = d_out;
+    K.n_views = n_views;
+    K.view_rows = K.n_local_bands * band_rows;
+    std::vector<float> v((size_t)n_views * 12, 0.0f);
+    for (int i = 0; i < n_views; ++i) {
+        float* o = v.data() + 12 * i;
+        for (int k = 0; k < 3; ++k) o[k] = cams[i].position[k];
+        for (int k = 0; k < 4; ++k) o[3 + k] = cams[i].quat[k];
+        o[7] = cams[i].half_height;
+        o[8] = cams[i].half_width;
+    }
+    rc = ensure(c, &c->d_views, &c->views_bytes, v.size() * sizeof(float));
+    if (rc != RT_OK) return rc;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    HIP_TRY(hipMemcpyAsync(c->d_views, v.data(), v.size() * sizeof(float), hipMemcpyHostToDevice, st));
+    K.views = reinterpret_cast<const float*>(c->d_views);
     return launch_render(c, K, st, g_count_mode, stats);
 }
 
@@ -1136,6 +1211,8 @@ extern "C" int rt_shade(rt_ctx* c, const rt_ray* rays, int n, const rt_params* p
         JobSrc J{};
         J.mode = 1;
         J.njobs = n;
+        J.n_views = 1;
+        J.view_jobs = n;
         J.rays = d_r;
         J.rgb = d_c;
         J.ray_counts = d_n;
@@ -1156,6 +1233,8 @@ extern "C" int rt_shade(rt_ctx* c, const rt_ray* rays, int n, const rt_params* p
         J.rays = d_r;
         J.rgb = d_c;
         J.ray_counts = d_n;
+        J.n_views = 1;
+        J.view_jobs = n;
         J.counter = reinterpret_cast<int*>(c->d_stats + 7);
         J.xq = use_xcd_queues() ? reinterpret_cast<int*>(c->d_stats + 16) : nullptr;
         hipMemsetAsync(c->d_stats, 0, RT_STATS_BYTES, c->stream);

@@ -110,11 +110,11 @@ assert RAY_DTYPE.itemsize == C.sizeof(rt_ray) and HIT_DTYPE.itemsize == C.sizeof
 
 # Every symbol include/rt_amd.h declares (checked by tests/test_abi.py).
 EXPORTS = [
-    "rt_abi_version", "rt_last_error", "rt_scene_new", "rt_scene_load_obj", "rt_scene_preset",
+    "rt_abi_version", "rt_device_count", "rt_last_error", "rt_scene_new", "rt_scene_load_obj", "rt_scene_preset",
     "rt_scene_add_sphere", "rt_scene_add_point_light", "rt_scene_add_spherical_light",
     "rt_scene_add_spot_light", "rt_scene_add_plane_light", "rt_scene_clear_lights", "rt_scene_set_material",
     "rt_scene_desc_get", "rt_scene_free", "rt_write_dragon_proxy", "rt_camera_from_trackball", "rt_create",
-    "rt_destroy", "rt_render", "rt_render_device", "rt_unpermute_bands_device", "rt_intersect", "rt_shade",
+    "rt_destroy", "rt_render", "rt_render_device", "rt_render_views_device", "rt_unpermute_bands_device", "rt_intersect", "rt_shade",
     "rt_set_counting", "rt_debug_counters", "rt_ctx_info", "rt_selftest_math",
     "rt_postprocess_device", "rt_bitmap_device", "rt_postprocess", "rt_bitmap", "rt_encode_bmp", "rt_write_bmp",
     "rt_philox4x32_10", "rt_debug_wave_trace", "rt_decode_png",
@@ -169,17 +169,32 @@ def encode_bmp(rgba, W, H):
 _lib = None
 
 
+def _torch_first():
+    """PyTorch wheels bundle their own HIP runtime.  Measured on the MI355X box: if librt_amd.so
+    (and /opt/rocm's runtime) is loaded before torch initialises the GPU, one of the two runtimes
+    later finds no device; with torch initialised first both work.  The drivers here (tests, bench,
+    smoke) use torch for buffers and streams, so initialise it before loading the library."""
+    try:
+        import torch
+    except ImportError:
+        return
+    if torch.cuda.is_available():
+        torch.cuda.init()
+
+
 def lib():
     """Load librt_amd.so (raises if it is missing: the product has no fallback)."""
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"{LIB_PATH} is missing: run __graft_entry__.build() (HIP path has no fallback)")
+        _torch_first()
         L = C.CDLL(LIB_PATH)
         P = C.POINTER
         vp = C.c_void_p
         sigs = {
             "rt_abi_version": ([], C.c_int),
+            "rt_device_count": ([C.POINTER(C.c_int)], C.c_int),
             "rt_last_error": ([C.c_char_p, C.c_size_t], C.c_int),
             "rt_scene_new": ([P(vp)], C.c_int),
             "rt_scene_load_obj": ([vp, C.c_char_p, C.c_int, C.c_int], C.c_int),
@@ -201,6 +216,8 @@ def lib():
             "rt_render": ([vp, P(rt_camera), P(rt_params), C.c_int, C.c_int, P(C.c_float), P(rt_stats)], C.c_int),
             "rt_render_device": ([vp, P(rt_camera), P(rt_params), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                   vp, vp, P(rt_stats)], C.c_int),
+            "rt_render_views_device": ([vp, P(rt_camera), C.c_int, P(rt_params), C.c_int, C.c_int, C.c_int, C.c_int,
+                                        C.c_int, vp, vp, P(rt_stats)], C.c_int),
             "rt_unpermute_bands_device": ([C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp], C.c_int),
             "rt_intersect": ([vp, vp, C.c_int, C.c_int, vp], C.c_int),
             "rt_shade": ([vp, vp, C.c_int, P(rt_params), P(C.c_float), P(C.c_uint64)], C.c_int),
@@ -327,6 +344,23 @@ def camera_from_trackball(look_at=(0.0, 0.0, 0.0), euler=None, distance=3.0, fov
 RADIANS = np.float32(0.01745329251994329576923690768489)
 
 
+def turntable_eulers(n, step_deg=None):
+    """Trackball Euler angles of n views orbiting the default view about the vertical axis
+    (Euler y = 20 deg + k * step), e.g. the frames of a turntable animation."""
+    step = 360.0 / max(1, n) if step_deg is None else step_deg
+    out = []
+    for k in range(n):
+        e = default_euler()
+        e[1] = float(np.float32(np.float32(20.0 + k * step) * RADIANS))
+        out.append(e)
+    return out
+
+
+def turntable_cameras(n, aspect, step_deg=None):
+    """Cameras of turntable_eulers(n), for one view batch (rt_render_views_device)."""
+    return [camera_from_trackball(euler=e, aspect=aspect) for e in turntable_eulers(n, step_deg)]
+
+
 def default_euler():
     """glm::radians(glm::vec3(20.0f, 20.0f, 0.0f)) (src/main.cpp:414), float32 multiply."""
     return [float(np.float32(20.0) * RADIANS), float(np.float32(20.0) * RADIANS), float(np.float32(0.0) * RADIANS)]
@@ -399,6 +433,15 @@ class Context:
         check(lib().rt_render_device(self.h, C.byref(cam), C.byref(prm), W, H, band_rows, band_rank, band_count,
                                      C.c_void_p(d_out_ptr), C.c_void_p(stream_ptr or 0), C.byref(st)),
               "rt_render_device")
+        return st
+
+    def render_views_device(self, cams, prm, W, H, band_rows, band_rank, band_count, d_out_ptr, stream_ptr=None):
+        """A batch of frames, one per camera, in one launch (rt_render_views_device); stats summed."""
+        arr = (rt_camera * len(cams))(*cams)
+        st = rt_stats()
+        check(lib().rt_render_views_device(self.h, arr, len(cams), C.byref(prm), W, H, band_rows, band_rank,
+                                           band_count, C.c_void_p(d_out_ptr), C.c_void_p(stream_ptr or 0),
+                                           C.byref(st)), "rt_render_views_device")
         return st
 
     def intersect(self, rays, use_bvh):

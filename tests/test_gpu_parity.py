@@ -224,3 +224,34 @@ def test_kernel_variants_bit_identical(R, ctxs, golden_dir, case):
                 os.environ.pop(k, None)
             else:
                 os.environ[k] = val
+
+
+@pytest.mark.parametrize("cfg,uv,kernel", [("C2", None, ""), ("C2", None, "df"), ("C3", (200, 80), ""),
+                                           ("C5", None, "")])
+def test_view_batch_bit_identical(R, O, ctxs, cfg, uv, kernel, monkeypatch):
+    """rt_render_views_device: every view of a batch is bit-identical to rt_render_device with that
+    camera (whole frame and band ranks), ray counts add up, and view 0 matches the oracle."""
+    import torch
+
+    if kernel:
+        monkeypatch.setenv("RT_KERNEL", kernel)
+    scene, ctx, prm, _, _ = ctxs(cfg, uv)
+    W, H = 100, 61  # ragged: a partial 8x8 tile column and a partial band
+    cams = R.turntable_cameras(5, R.aspect_of(W, H))
+    for rank, count in ((0, 1), (1, 3)):
+        n = R.local_band_elems(W, H, 8, count)
+        batch = torch.full((len(cams) * n,), -1.0, dtype=torch.float32, device="cuda")
+        st = ctx.render_views_device(cams, prm, W, H, 8, rank, count, batch.data_ptr(), None)
+        torch.cuda.synchronize()
+        rays = 0
+        for v, cam in enumerate(cams):
+            one = torch.full((n,), -1.0, dtype=torch.float32, device="cuda")
+            s = ctx.render_device(cam, prm, W, H, 8, rank, count, one.data_ptr(), None)
+            torch.cuda.synchronize()
+            rays += s.rays
+            assert batch[v * n:(v + 1) * n].cpu().numpy().tobytes() == one.cpu().numpy().tobytes(), (v, rank)
+        assert st.rays == rays
+    img, st1 = ctx.render(cams[2], prm, W, H)
+    ref, rays = O.Oracle(scene).render(prm, W, H, euler=R.turntable_eulers(5)[2])
+    assert st1.rays == rays
+    assert float(np.max(np.abs(img - ref))) <= TOL

@@ -1,13 +1,26 @@
-"""rocprofv3 target: build one config's scene, then render it N times (same launches bench.py times)."""
+"""rocprofv3 target: build one config's scene, then render it N times -- the same launches bench.py
+times: one frame (views = 1) or a turntable batch of V views in one launch (bench.py --views V).
+
+    python tools/prof_target.py CONFIG N [VIEWS]
+"""
 import os, sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "raytracer-group27_amd"))
 import rt_amd as R
 cfg = sys.argv[1] if len(sys.argv) > 1 else "C3"
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+views = int(sys.argv[3]) if len(sys.argv) > 3 else 1
 s, p, W, H, desc = R.build_config(cfg)
 ctx = R.Context(s)
-cam = R.camera_from_trackball(aspect=R.aspect_of(W, H))
-for _ in range(n):
-    img, st = ctx.render(cam, p, W, H)
-print(cfg, "rays", st.rays, "kernel_ms", st.kernel_ms, flush=True)
+if views == 1:
+    cam = R.camera_from_trackball(aspect=R.aspect_of(W, H))
+    for _ in range(n):
+        img, st = ctx.render(cam, p, W, H)
+else:
+    import torch
+    cams = R.turntable_cameras(views, R.aspect_of(W, H))
+    buf = torch.zeros(views * R.local_band_elems(W, H, 8, 1), dtype=torch.float32, device="cuda")
+    for _ in range(n):
+        st = ctx.render_views_device(cams, p, W, H, 8, 0, 1, buf.data_ptr(), None)
+    torch.cuda.synchronize()
+print(cfg, "views", views, "rays", st.rays, "kernel_ms", st.kernel_ms, flush=True)
