@@ -2,7 +2,7 @@
 
 Workload (config.workload): C3 = dragon proxy (800 000 triangles), 1920x1080,
 one point light, hard shadows + mirror recursion depth 4 (BASELINE.json configs[2]).  One step
-renders a batch of --views full frames (default 8: a turntable of the scene, 45 degrees apart) in
+renders a batch of --views full frames (default 16: a turntable of the scene, 22.5 degrees apart) in
 ONE launch of the persistent kernel (rt_render_views_device), each frame un-permuted into its own
 Screen::m_textureData image; every rank renders its own batch (weak scaling, no collective on the
 data path).  --views 1 renders one frame per step; --partition bands splits one frame over the
@@ -28,7 +28,7 @@ import numpy as np  # noqa: E402
 METRIC = "Mrays/s (primary+shadow+secondary) at 1920×1080; fraction of HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 BAND_ROWS = 8
-DEFAULT_VIEWS = 8  # frames per step: an 8-view turntable (45 deg apart) of the C3 scene in one launch
+DEFAULT_VIEWS = 16  # frames per step: a 16-view turntable (22.5 deg apart) of the C3 scene in one launch
 
 
 def algorithmic_bytes(st, pixels):
@@ -126,7 +126,7 @@ def main():
                          "on the data path); bands = one frame split into interleaved 8-row bands, RCCL "
                          "all-gather, un-permute on rank 0 (strong scaling, single-frame latency)")
     ap.add_argument("--views", type=int, default=None,
-                    help="frames per step (default 8; 1 with --partition bands): a turntable batch of this many "
+                    help="frames per step (default 16; 1 with --partition bands): a turntable batch of this many "
                          "views of the scene rendered in ONE launch (rt_render_views_device; the drain tail of one "
                          "frame overlaps the next), every frame un-permuted into its own Screen-layout image")
     ap.add_argument("--view-step", type=float, default=None,
