@@ -1719,7 +1719,8 @@ __global__ __launch_bounds__(64, WPE) void persistent_df_kernel(KParams P, JobSr
                     lanes_drain += (unsigned int)__popcll(__ballot(tracing));
                 }
                 // drain (no lane can take a new job): the remaining queries go to lane groups
-                if (P.coop && !__any(L.job == -1) && __any(L.job == -2)) {
+                // (coop 2: also in steady state, for the last queries a full-wave refill waits for)
+                if (P.coop && ((P.coop == 2 && refill_at == 64) || (!__any(L.job == -1) && __any(L.job == -2)))) {
                     const unsigned long long om = __ballot(tracing);
                     const int k = __popcll(om);
                     if (k <= P.coop_max) {

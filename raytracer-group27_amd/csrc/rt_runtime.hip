@@ -653,7 +653,7 @@ static int fill_params(rt_ctx* c, const rt_camera* cam, const rt_params* p, int 
     K.refill = refill_threshold();
     {
         const char* cp = std::getenv("RT_COOP");  // drain-phase cooperative traversal (default on)
-        K.coop = (cp && cp[0] == '0') ? 0 : 1;
+        K.coop = (cp && cp[0] == '0') ? 0 : ((cp && cp[0] == '2') ? 2 : 1);
         // a group of G lanes owns COOP_POOL * G / 64 pool slots: the depth-first reserve plus one
         // breadth step must fit; coop_max = the largest query count whose groups still do
         K.coop_reserve = 7 * (c->bvh8_depth + 1) + 8;
@@ -1067,6 +1067,15 @@ extern "C" int rt_render_device(rt_ctx* c, const rt_camera* cam, const rt_params
     K.band_count = band_count;
     K.n_local_bands = nbands > band_rank ? (nbands - band_rank + band_count - 1) / band_count : 0;
     K.out = d_out;
+    // Few shadow samples per shading point (point/spot lights: long mirror and camera queries):
+    // full-wave refill + lane groups for the stragglers (C3 2.37 -> 2.18 ms).  Sample-heavy
+    // lights (sphere/plane lights, many short shadow queries) keep the 24-lane refill (C4 43.6 ms
+    // against 48.5 ms with it).
+    if (!std::getenv("RT_REFILL") && !std::getenv("RT_COOP") && K.coop == 1 &&
+        K.S.nsl * K.sl_count + K.S.nplane * K.plane_k * K.plane_k <= 4) {
+        K.refill = 64;
+        K.coop = 2;
+    }
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     return launch_render(c, K, st, g_count_mode, stats);
 }
@@ -1102,8 +1111,10 @@ extern "C" int rt_render_views_device(rt_ctx* c, const rt_camera* cams, int n_vi
     K.out = d_out;
     // dynamic-fetch refill threshold: in a batch only the last frame drains, and advancing all 64
     // lanes at once amortises the state machine's spills best (C3, 8 views: 24 -> 64 lanes = 1.59 ->
-    // 1.37 ms/frame; single frames keep 24, where the drain dominates: C3 2.35 vs 2.48 ms)
+    // 1.37 ms/frame); the last queries a full-wave refill waits for go to lane groups (coop 2:
+    // C3, 16 views, 1.29 -> 1.17 ms/frame; C4 neutral)
     if (!std::getenv("RT_REFILL")) K.refill = 64;
+    if (!std::getenv("RT_COOP") && K.coop == 1) K.coop = 2;
     K.n_views = n_views;
     K.view_rows = K.n_local_bands * band_rows;
     std::vector<float> v((size_t)n_views * 12, 0.0f);

@@ -1,6 +1,7 @@
 """Developer tool: SIMD efficiency of the persistent kernels from the counting build.
 Per config and variant: lane node visits / (64 x wave node steps), same for triangle records
-and for state-machine advances (one per query).  Usage: python tools/simd_eff.py C3 old:RT_KERNEL=persistent df:"""
+and for state-machine advances (one per query).  Usage: python tools/simd_eff.py C3 old:RT_KERNEL=persistent df:
+SE_VIEWS=V renders a turntable batch of V views in one launch (rt_render_views_device) instead of one frame."""
 import os
 import sys
 
@@ -17,12 +18,20 @@ for cfg in cfgs:
     s, p, W, H, desc = R.build_config(cfg)
     ctx = R.Context(s)
     cam = R.camera_from_trackball(aspect=R.aspect_of(W, H))
+    V = int(os.environ.get("SE_VIEWS", "1"))
+    if V > 1:
+        import torch
+        cams = R.turntable_cameras(V, R.aspect_of(W, H))
+        buf = torch.zeros(V * R.local_band_elems(W, H, 8, 1), dtype=torch.float32, device="cuda")
     for name, env in variants:
         for k in keys:
             os.environ.pop(k, None)
         os.environ.update(env)
         R.set_counting(True)
-        _, st = ctx.render(cam, p, W, H)
+        if V > 1:
+            st = ctx.render_views_device(cams, p, W, H, 8, 0, 1, buf.data_ptr(), None)
+        else:
+            _, st = ctx.render(cam, p, W, H)
         R.set_counting(False)
         c = ctx.debug_counters()
         rays, nodes, tris, hits, wn, wt, wa = (int(x) for x in c[:7])
