@@ -226,16 +226,21 @@ def test_kernel_variants_bit_identical(R, ctxs, golden_dir, case):
                 os.environ[k] = val
 
 
-@pytest.mark.parametrize("cfg,uv,kernel", [("C2", None, ""), ("C2", None, "df"), ("C3", (200, 80), ""),
-                                           ("C5", None, "")])
-def test_view_batch_bit_identical(R, O, ctxs, cfg, uv, kernel, monkeypatch):
+@pytest.mark.parametrize("cfg,uv,kernel,aa", [("C2", None, "", 0), ("C2", None, "df", 0), ("C2", None, "df", 1),
+                                              ("C3", (200, 80), "", 0), ("C4", (200, 80), "", 0),
+                                              ("C5", None, "", 0)])
+def test_view_batch_bit_identical(R, O, ctxs, cfg, uv, kernel, aa, monkeypatch):
     """rt_render_views_device: every view of a batch is bit-identical to rt_render_device with that
-    camera (whole frame and band ranks), ray counts add up, and view 0 matches the oracle."""
+    camera (whole frame and band ranks; the batch runs its own refill / lane-group defaults), ray
+    counts add up, and a rotated view matches the oracle."""
     import torch
 
     if kernel:
         monkeypatch.setenv("RT_KERNEL", kernel)
     scene, ctx, prm, _, _ = ctxs(cfg, uv)
+    if aa:
+        prm = type(prm).from_buffer_copy(prm)
+        prm.anti_aliasing = 1
     W, H = 100, 61  # ragged: a partial 8x8 tile column and a partial band
     cams = R.turntable_cameras(5, R.aspect_of(W, H))
     for rank, count in ((0, 1), (1, 3)):
