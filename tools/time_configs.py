@@ -1,4 +1,5 @@
-"""Developer tool: full-size GPU render time + ray count of every BASELINE config (one GPU)."""
+"""Developer tool: full-size GPU render time + ray count of every BASELINE config (one GPU), one
+frame per launch and (TC_VIEWS=V, default 8; 0 = skip) a turntable batch of V views in one launch."""
 import os
 import sys
 import time
@@ -23,4 +24,14 @@ for cfg in cfgs:
     print(f"{cfg} {desc}: load {t1 - t0:.2f}s upload+bvh {t2 - t1:.2f}s kernel {st.kernel_ms:.2f} ms rays {st.rays} "
           f"-> {st.rays / st.kernel_ms / 1e3:.1f} Mrays/s | nodes/ray {cst.node_visits / cst.rays:.1f} "
           f"tris/ray {cst.tri_tests / cst.rays:.1f} hits {cst.hits}", flush=True)
+    V = int(os.environ.get("TC_VIEWS", "8"))
+    if V > 1:
+        import torch
+        cams = R.turntable_cameras(V, R.aspect_of(W, H))
+        buf = torch.zeros(V * R.local_band_elems(W, H, 8, 1), dtype=torch.float32, device="cuda")
+        ctx.render_views_device(cams, p, W, H, 8, 0, 1, buf.data_ptr(), None)
+        vst = ctx.render_views_device(cams, p, W, H, 8, 0, 1, buf.data_ptr(), None)
+        print(f"{cfg} batch of {V} views: kernel {vst.kernel_ms:.2f} ms = {vst.kernel_ms / V:.2f} ms/frame, rays "
+              f"{vst.rays} -> {vst.rays / vst.kernel_ms / 1e3:.1f} Mrays/s", flush=True)
+        del buf
     ctx.close()
