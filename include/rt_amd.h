@@ -14,6 +14,7 @@
  *                        src/main.cpp:340-400 (+ Screen::setPixel src/screen.cpp:32-38)
  *   rt_render_device     same as rt_render, band-partitioned, device-resident output (multi-GPU path)
  *   rt_render_views_device  a batch of rt_render_device frames (one camera each) in one launch
+ *   rt_render_views      the same batch, host output in the rt_render layout
  *   rt_camera_from_trackball  Trackball::generateRay / position(), framework/src/trackball.cpp:65-98
  *   rt_scene_load_obj    std::vector<Mesh> loadMesh(path, bool normalize), src/mesh.cpp:58-188
  *   rt_scene_preset      Scene loadScene(SceneType, dataDir), src/scene.cpp:4-150
@@ -256,6 +257,11 @@ int rt_render_device(rt_ctx* ctx, const rt_camera* cam, const rt_params* params,
 int rt_render_views_device(rt_ctx* ctx, const rt_camera* cams, int n_views, const rt_params* params,
                            int width, int height, int band_rows, int band_rank, int band_count,
                            float* d_rgb_out, void* stream, rt_stats* stats);
+/* View batch to host memory: rgb_out = n_views frames of W*H*3 floats, each in Screen::m_textureData
+ * order (the rt_render layout), view v at v*W*H*3.  Same kernel and results as
+ * rt_render_views_device; stats summed over the views. */
+int rt_render_views(rt_ctx* ctx, const rt_camera* cams, int n_views, const rt_params* params, int width,
+                    int height, float* rgb_out, rt_stats* stats);
 /* Un-permute gathered band buffers ([band_count][max_local_bands][band_rows][W][3]) into the
  * setPixel layout on the device. */
 int rt_unpermute_bands_device(int width, int height, int band_rows, int band_count,

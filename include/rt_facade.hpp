@@ -10,6 +10,7 @@
 //                                                       rt::facade::BoundingVolumeHierarchy
 //   getFinalColor (src/main.cpp:129)                    rt::facade::getFinalColor
 //   renderRayTracing (src/main.cpp:340)                 rt::facade::renderRayTracing
+//   one renderRayTracing per camera, batched             rt::facade::renderRayTracingViews
 //
 // Errors: loadMesh/loadScene throw std::runtime_error like the reference's loadMesh throws
 // (src/mesh.cpp:60-73); intersect() never throws and returns false on a miss.  A device error
@@ -240,6 +241,31 @@ inline void renderRayTracing(const Trackball& cam, const BoundingVolumeHierarchy
     p.sample_size = sampleSize;
     screen.resize((size_t)W * H * 3);
     check(rt_render(bvh.handle(), &c, &p, W, H, screen.data(), nullptr), "renderRayTracing");
+}
+
+// A batch of renderRayTracing calls, one per camera (a turntable, an animation's camera path), in ONE
+// launch of the persistent kernel (rt_render_views): screens[v] = the frame of cams[v], bit-identical to
+// renderRayTracing(cams[v], ...).
+inline void renderRayTracingViews(const std::vector<Trackball>& cams, const BoundingVolumeHierarchy& bvh, int W,
+                                  int H, std::vector<std::vector<float>>& screens, bool anti_aliasing = false,
+                                  bool multipleRays = false, int sampleSize = 4, const RenderSettings& s = {}) {
+    std::vector<rt_camera> c(cams.size());
+    for (size_t v = 0; v < cams.size(); ++v) {
+        const Trackball& t = cams[v];
+        const float la[3] = {t.lookAt.x, t.lookAt.y, t.lookAt.z};
+        const float eu[3] = {t.rotationEulerAngles.x, t.rotationEulerAngles.y, t.rotationEulerAngles.z};
+        check(rt_camera_from_trackball(la, eu, t.distance, t.fovy, float(W) / float(H), &c[v]), "camera");
+    }
+    rt_params p = s.to_c();
+    p.anti_aliasing = anti_aliasing ? 1 : 0;
+    p.multiple_rays = multipleRays ? 1 : 0;
+    p.sample_size = sampleSize;
+    const size_t frame = (size_t)W * H * 3;
+    std::vector<float> all(frame * cams.size());
+    check(rt_render_views(bvh.handle(), c.data(), (int)c.size(), &p, W, H, all.data(), nullptr),
+          "renderRayTracingViews");
+    screens.assign(cams.size(), {});
+    for (size_t v = 0; v < cams.size(); ++v) screens[v].assign(all.begin() + v * frame, all.begin() + (v + 1) * frame);
 }
 
 // class Screen (src/screen.h:32-161): the framebuffer renderRayTracing fills, with the

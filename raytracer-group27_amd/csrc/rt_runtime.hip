@@ -1173,6 +1173,34 @@ extern "C" int rt_render(rt_ctx* c, const rt_camera* cam, const rt_params* p, in
     return RT_OK;
 }
 
+extern "C" int rt_render_views(rt_ctx* c, const rt_camera* cams, int n_views, const rt_params* p, int W, int H,
+                               float* rgb_out, rt_stats* stats) {
+    if (!c || !cams || n_views <= 0 || !p || !rgb_out || W <= 0 || H <= 0) {
+        set_error("rt_render_views: invalid argument");
+        return RT_ERR_INVALID;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    const int band_rows = 8;
+    const int nbands = (H + band_rows - 1) / band_rows;
+    const size_t view_fb = (size_t)nbands * band_rows * W * 3;
+    const size_t view_img = (size_t)W * H * 3;
+    int rc = ensure(c, &c->d_fb, &c->fb_bytes, view_fb * n_views * sizeof(float));
+    if (rc != RT_OK) return rc;
+    rc = ensure(c, &c->d_img, &c->img_bytes, view_img * n_views * sizeof(float));
+    if (rc != RT_OK) return rc;
+    rt_stats local{};
+    rc = rt_render_views_device(c, cams, n_views, p, W, H, band_rows, 0, 1, c->d_fb, c->stream, &local);
+    if (rc != RT_OK) return rc;
+    for (int v = 0; v < n_views; ++v) {
+        rc = rt_unpermute_bands_device(W, H, band_rows, 1, c->d_fb + v * view_fb, c->d_img + v * view_img, c->stream);
+        if (rc != RT_OK) return rc;
+    }
+    HIP_TRY(hipMemcpyAsync(rgb_out, c->d_img, view_img * n_views * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (stats) *stats = local;
+    return RT_OK;
+}
+
 extern "C" int rt_intersect(rt_ctx* c, const rt_ray* rays, int n, int use_bvh, rt_hit* hits) {
     if (!c || n < 0 || (n > 0 && (!rays || !hits))) {
         set_error("rt_intersect: invalid argument");

@@ -114,7 +114,7 @@ EXPORTS = [
     "rt_scene_add_sphere", "rt_scene_add_point_light", "rt_scene_add_spherical_light",
     "rt_scene_add_spot_light", "rt_scene_add_plane_light", "rt_scene_clear_lights", "rt_scene_set_material",
     "rt_scene_desc_get", "rt_scene_free", "rt_write_dragon_proxy", "rt_camera_from_trackball", "rt_create",
-    "rt_destroy", "rt_render", "rt_render_device", "rt_render_views_device", "rt_unpermute_bands_device", "rt_intersect", "rt_shade",
+    "rt_destroy", "rt_render", "rt_render_device", "rt_render_views_device", "rt_render_views", "rt_unpermute_bands_device", "rt_intersect", "rt_shade",
     "rt_set_counting", "rt_debug_counters", "rt_ctx_info", "rt_selftest_math",
     "rt_postprocess_device", "rt_bitmap_device", "rt_postprocess", "rt_bitmap", "rt_encode_bmp", "rt_write_bmp",
     "rt_philox4x32_10", "rt_debug_wave_trace", "rt_decode_png",
@@ -218,6 +218,8 @@ def lib():
                                   vp, vp, P(rt_stats)], C.c_int),
             "rt_render_views_device": ([vp, P(rt_camera), C.c_int, P(rt_params), C.c_int, C.c_int, C.c_int, C.c_int,
                                         C.c_int, vp, vp, P(rt_stats)], C.c_int),
+            "rt_render_views": ([vp, P(rt_camera), C.c_int, P(rt_params), C.c_int, C.c_int, P(C.c_float),
+                                 P(rt_stats)], C.c_int),
             "rt_unpermute_bands_device": ([C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp], C.c_int),
             "rt_intersect": ([vp, vp, C.c_int, C.c_int, vp], C.c_int),
             "rt_shade": ([vp, vp, C.c_int, P(rt_params), P(C.c_float), P(C.c_uint64)], C.c_int),
@@ -434,6 +436,15 @@ class Context:
                                      C.c_void_p(d_out_ptr), C.c_void_p(stream_ptr or 0), C.byref(st)),
               "rt_render_device")
         return st
+
+    def render_views(self, cams, prm, W, H):
+        """A batch of frames to host memory (rt_render_views): float32 [n_views, W*H*3], stats summed."""
+        arr = (rt_camera * len(cams))(*cams)
+        out = np.zeros((len(cams), W * H * 3), np.float32)
+        st = rt_stats()
+        check(lib().rt_render_views(self.h, arr, len(cams), C.byref(prm), W, H,
+                                    out.ctypes.data_as(C.POINTER(C.c_float)), C.byref(st)), "rt_render_views")
+        return out, st
 
     def render_views_device(self, cams, prm, W, H, band_rows, band_rank, band_count, d_out_ptr, stream_ptr=None):
         """A batch of frames, one per camera, in one launch (rt_render_views_device); stats summed."""

@@ -27,6 +27,19 @@ int main(int argc, char** argv) {
         double sum = 0;
         for (float v : screen) sum += v;
         std::printf("frame_sum=%.9g\n", sum);
+        // a turntable batch: every view equals its own renderRayTracing call, bit for bit
+        std::vector<Trackball> cams(3);
+        cams[1].rotationEulerAngles.y += 0.5f;
+        cams[2].rotationEulerAngles.y += 1.0f;
+        std::vector<std::vector<float>> views;
+        renderRayTracingViews(cams, bvh, 32, 32, views);
+        int same = 0;
+        for (size_t v = 0; v < cams.size(); ++v) {
+            std::vector<float> one;
+            renderRayTracing(cams[v], bvh, 32, 32, one);
+            same += (one == views[v]) ? 1 : 0;
+        }
+        std::printf("views_identical=%d/%d\n", same, (int)cams.size());
         // Screen + bloom + gamma + BMP, as the "Render to file" button does (src/main.cpp:513-522)
         Screen scr(32, 24);
         scr.setBloomFilter(FilteringOption::BloomWithReinhardHdr);

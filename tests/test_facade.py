@@ -35,5 +35,6 @@ def test_facade_runs_on_gpu(R, tmp_path):
     r = subprocess.run([exe, R.data_dir(), bmp], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "hit=1" in r.stdout and "frame_sum=" in r.stdout
+    assert "views_identical=3/3" in r.stdout, r.stdout
     data = open(bmp, "rb").read()
     assert data[:2] == b"BM" and len(data) == 54 + 32 * 3 * 24

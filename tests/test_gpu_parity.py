@@ -256,6 +256,13 @@ def test_view_batch_bit_identical(R, O, ctxs, cfg, uv, kernel, aa, monkeypatch):
             rays += s.rays
             assert batch[v * n:(v + 1) * n].cpu().numpy().tobytes() == one.cpu().numpy().tobytes(), (v, rank)
         assert st.rays == rays
+    host, sth = ctx.render_views(cams, prm, W, H)  # rt_render_views: host output, rt_render layout
+    hrays = 0
+    for v, cam in enumerate(cams):
+        one, s = ctx.render(cam, prm, W, H)
+        hrays += s.rays
+        assert host[v].tobytes() == one.tobytes(), v
+    assert sth.rays == hrays
     img, st1 = ctx.render(cams[2], prm, W, H)
     ref, rays = O.Oracle(scene).render(prm, W, H, euler=R.turntable_eulers(5)[2])
     assert st1.rays == rays
