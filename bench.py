@@ -141,7 +141,15 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # BENCH_DIST_BACKEND=gloo: rehearsal of the N-rank path with several ranks on one GPU (RCCL
+        # refuses two ranks on one device); the driver's multi-GPU runs use RCCL ("nccl")
+        backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    if local >= torch.cuda.device_count():  # rehearsal: more ranks than GPUs share the visible ones
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 

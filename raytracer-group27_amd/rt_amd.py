@@ -539,9 +539,11 @@ def data_dir():
         dst = os.path.join(out, f[:-3])
         src = os.path.join(SCENE_DIR, f)
         if not os.path.exists(dst) or os.path.getmtime(dst) < os.path.getmtime(src):
-            with gzip.open(src, "rb") as fi, open(dst + ".tmp", "wb") as fo:
+            # per-process temporary: ranks of one node expand the same files concurrently
+            tmp = f"{dst}.{os.getpid()}.tmp"
+            with gzip.open(src, "rb") as fi, open(tmp, "wb") as fo:
                 shutil.copyfileobj(fi, fo)
-            os.replace(dst + ".tmp", dst)
+            os.replace(tmp, dst)
     return out
 
 

@@ -74,3 +74,37 @@ def test_band_rows_cover_image_once():
     for H, br, n in [(1080, 8, 8), (1080, 8, 3), (2160, 8, 7), (5, 8, 2)]:
         rows = [r for k in range(n) for r in R.band_rows_of(H, br, k, n)]
         assert sorted(rows) == list(range(H))
+
+
+def _expand_scenes(cache, q):
+    import os
+    import sys
+
+    os.environ["RT_SCENE_CACHE"] = cache
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "raytracer-group27_amd"))
+    try:
+        import rt_amd
+
+        d = rt_amd.data_dir()
+        q.put(sorted(os.listdir(d)))
+    except Exception as e:  # noqa: BLE001
+        q.put(repr(e))
+
+
+def test_ranks_expand_scene_cache_concurrently(tmp_path):
+    """Every rank of a node expands the gzipped reference scenes into the same cache directory at
+    start-up (bench.py on N GPUs): concurrent expansion must not collide."""
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    cache = str(tmp_path / "scenes")
+    ps = [ctx.Process(target=_expand_scenes, args=(cache, q)) for _ in range(6)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+    assert all(isinstance(r, list) for r in res), res
+    assert all(r == res[0] for r in res)
+    assert not [f for f in res[0] if f.endswith(".tmp")]
