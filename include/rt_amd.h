@@ -18,13 +18,19 @@
  *   rt_camera_from_trackball  Trackball::generateRay / position(), framework/src/trackball.cpp:65-98
  *   rt_scene_load_obj    std::vector<Mesh> loadMesh(path, bool normalize), src/mesh.cpp:58-188
  *   rt_scene_preset      Scene loadScene(SceneType, dataDir), src/scene.cpp:4-150
+ *   rt_update_lights     the ImGui light editors after the BVH exists, src/main.cpp:511-613
+ *   rt_update_materials  material edits (scene.meshes[i].material), no BVH rebuild
+ *   rt_texture_sample    Image::getPixel(texCoord, lod), src/image.cpp:77-110 (parity tests)
  *   rt_destroy           ~BoundingVolumeHierarchy / scene teardown
  *
  * Conventions: plain pointers and sizes, no C++ or torch types.  Every function returns an
  * int status: 0 = ok, < 0 = error (message via rt_last_error).  The caller owns every host
- * buffer it passes; a context owns its device memory.  Calls on one context are synchronous
- * and must not be made concurrently (the reference BVH is shared read-only by OpenMP threads;
- * here the parallelism is inside the GPU launch).
+ * buffer it passes; a context owns its device memory.  Calls on one context must not be made
+ * concurrently (the reference BVH is shared read-only by OpenMP threads; here the parallelism is
+ * inside the GPU launch).  The *_device calls are asynchronous on the caller's stream unless
+ * `stats` is given; a context keeps ONE set of per-render scratch (camera table, job counters), so
+ * its renders must be ordered on one stream (or separated by events) -- two renders of one
+ * context in flight on different streams at once would share that scratch.
  */
 #ifndef RT_AMD_H
 #define RT_AMD_H
@@ -36,7 +42,8 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 3  /* 2: textures (rt_texture, rt_params texture fields); 3: rt_render_views_device */
+#define RT_ABI_VERSION 4  /* 2: textures; 3: rt_render_views_device; 4: rt_stats.ub_hits / .kernel,
+                             rt_ctx_set_option, rt_update_lights / _materials, rt_texture_sample */
 
 /* status codes */
 #define RT_OK 0
@@ -180,10 +187,12 @@ typedef struct rt_stats {
     uint64_t node_visits;   /* BVH nodes fetched (counting builds only, else 0) */
     uint64_t tri_tests;     /* triangle records fetched (counting builds only, else 0) */
     uint64_t hits;          /* closest hits shaded (counting builds only, else 0) */
-    float kernel_ms;        /* device time of the render launch(es), HIP events */
-    uint32_t node_bytes;    /* bytes per node record of the BVH walked: 64 (BVH2), 128 (quantised BVH8) */
-    float trace_ms;         /* wavefront path: device time of the trace launches (HIP events), else 0 */
-    uint32_t trace_launches;/* wavefront path: trace launches of the frame */
+    uint64_t ub_hits;       /* counting builds: shaded triangle hits where the reference's
+                               barycentricCoordinates returns false (src/ray_tracing.cpp:281-295) and it
+                               interpolates from uninitialised coordinates (:147-157) */
+    float kernel_ms;        /* device time of the render launch, HIP events */
+    uint32_t node_bytes;    /* bytes per node record of the BVH walked: 128 (quantised BVH8) */
+    char kernel[64];        /* the render kernel launched, as rocprofv3 names it (without its argument list) */
 } rt_stats;
 
 typedef struct rt_ctx rt_ctx;
@@ -251,8 +260,7 @@ int rt_render_device(rt_ctx* ctx, const rt_camera* cam, const rt_params* params,
  * spans every view, so the drain tail of one frame overlaps the start of the next.  d_rgb_out
  * holds n_views rt_render_device buffers back to back (view v at v * n_local_bands * band_rows *
  * width * 3 floats); view v's buffer is bit-identical to rt_render_device with cams[v].  Stats
- * are summed over the views.  Persistent kernels only (RT_KERNEL=tile/wavefront, RT_PACKET=1 and
- * RT_SCHED are rejected with RT_ERR_INVALID).  n_views == 1 is rt_render_device.
+ * are summed over the views.  n_views == 1 is rt_render_device.
  */
 int rt_render_views_device(rt_ctx* ctx, const rt_camera* cams, int n_views, const rt_params* params,
                            int width, int height, int band_rows, int band_rank, int band_count,
@@ -267,16 +275,45 @@ int rt_render_views(rt_ctx* ctx, const rt_camera* cams, int n_views, const rt_pa
 int rt_unpermute_bands_device(int width, int height, int band_rows, int band_count,
                               const float* d_gathered, float* d_image, void* stream);
 
+/* Un-permute a view batch gathered from band_count ranks -- each rank's rt_render_views_device
+ * buffer ([n_views][max_local_bands][band_rows][W][3]) back to back, rank after rank -- into n_views
+ * images of W*H*3 floats in the setPixel layout (the multi-GPU tile split of a batch; one launch). */
+int rt_unpermute_views_device(int width, int height, int band_rows, int band_count, int n_views,
+                              const float* d_gathered, float* d_images, void* stream);
+
 /* Per-ray entry points used by the facade and the parity tests (host buffers). */
 int rt_intersect(rt_ctx* ctx, const rt_ray* rays, int n, int use_bvh, rt_hit* hits);
 int rt_shade(rt_ctx* ctx, const rt_ray* rays, int n, const rt_params* params, float* rgb,
              uint64_t* rays_per_sample);
+/* Image::getPixel (src/image.cpp:77-110) of texture `texture` for n (u, v, lod) triples, under the
+ * params' texture_filtering / out_of_bounds rules / border colour: rgb = n * 3 floats. */
+int rt_texture_sample(rt_ctx* ctx, int texture, int n, const float* uv_lod, const rt_params* params, float* rgb);
 
-/* Counting build of the same kernel (node visits, triangle records, hits) for roofline accounting. */
+/* Edits after upload.  rt_update_lights replaces the context's four light arrays with desc's (only
+ * the light fields of desc are read).  rt_update_materials replaces every mesh material and every
+ * sphere material (counts must match the scene; texture bindings are fixed at rt_create). */
+int rt_update_lights(rt_ctx* ctx, const rt_scene_desc* desc);
+int rt_update_materials(rt_ctx* ctx, int num_meshes, const rt_material* materials, int num_spheres,
+                        const rt_material* sphere_materials);
+
+/* Counting build of the same kernel (node visits, triangle records, hits, UB-regime hits) for
+ * roofline accounting (process-wide switch). */
 int rt_set_counting(int on);
-/* Debug counters of the last counting launch (per-query node-visit histogram, maxima). */
+/* Developer counters of the last counting launch (16 words; [8..11] state-machine / traversal clocks). */
 int rt_debug_counters(rt_ctx* ctx, uint64_t* out, int n);
-/* Developer wave trace of the last persistent-kernel launch made with RT_WAVE_TRACE=1: 8 words
+/* Context options: test and developer hooks (the library reads no environment variables).  The
+ * defaults are the shipped path; every setting renders the same image and ray count. */
+#define RT_OPT_KERNEL 1      /* RT_KERNEL_AUTO (by scene size), _WHOLE_TRAVERSAL or _DYNAMIC_FETCH */
+#define RT_OPT_COOP 2        /* drain lane groups: -1 by render shape, 0 off, 1 drain only, 2 + full-wave stragglers */
+#define RT_OPT_COOP_MAX 3    /* most queries handed to lane groups (0: as many as the LDS pool allows) */
+#define RT_OPT_REFILL 4      /* dynamic-fetch kernel: waiting lanes that end a traversal phase (0: by shape) */
+#define RT_OPT_WAVE_TRACE 5  /* 1: record rt_debug_wave_trace data */
+#define RT_OPT_VARIANT 6     /* developer A/B: compiled kernel variant (rt_megakernel.hip RT_V_*), -1 default */
+#define RT_KERNEL_AUTO 0
+#define RT_KERNEL_WHOLE_TRAVERSAL 1
+#define RT_KERNEL_DYNAMIC_FETCH 2
+int rt_ctx_set_option(rt_ctx* ctx, int option, int value);
+/* Developer wave trace of the last persistent-kernel launch made with RT_OPT_WAVE_TRACE = 1: 8 words
  * per wave (start, end, jobs taken, time the job queue ran dry for it, drain iterations, sum of
  * tracing lanes over them, 0, drain state-machine passes); timestamps of
  * the 100 MHz device clock.  Out holds 8 * max_waves words.  Returns the wave count. */

@@ -38,10 +38,12 @@ def lib():
         L.oracle_shade.argtypes = [vp, vp, C.c_int, vp, F3, C.POINTER(C.c_uint64)]
         L.oracle_camera.argtypes = [F3, F3, C.c_float, C.c_float, C.c_float, F3]
         L.oracle_render_pixels.argtypes = [vp, F3, F3, C.c_float, C.c_float, C.c_int, C.c_int, vp,
-                                           C.POINTER(C.c_int), C.c_int, F3, C.POINTER(C.c_uint64)]
+                                           C.POINTER(C.c_int), C.c_int, F3, C.POINTER(C.c_uint64),
+                                           C.POINTER(C.c_uint64)]
         L.oracle_render.argtypes = [vp, F3, F3, C.c_float, C.c_float, C.c_int, C.c_int, vp, F3,
                                     C.POINTER(C.c_uint64)]
         L.oracle_set_threads.argtypes = [C.c_int]
+        L.oracle_tex_sample.argtypes = [vp, C.c_int, F3, C.c_int, vp, F3]
         U3 = C.POINTER(C.c_uint32)
         L.oracle_philox.argtypes = [U3, U3, U3]
         L.oracle_postprocess.argtypes = [vp, C.c_int, C.c_int, F3]
@@ -90,6 +92,15 @@ class Oracle:
                            cnt.ctypes.data_as(C.POINTER(C.c_uint64)))
         return rgb.reshape(-1, 3), cnt
 
+    def texture_sample(self, texture, uv_lod, prm):
+        """Image::getPixel(uv, lod) for rows (u, v, lod); returns [n, 3] float32."""
+        a = np.ascontiguousarray(uv_lod, np.float32).reshape(-1, 3)
+        out = np.zeros((len(a), 3), np.float32)
+        rc = lib().oracle_tex_sample(self.h, int(texture), _fp(a), len(a), C.addressof(prm), _fp(out))
+        if rc != 0:
+            raise ValueError(f"no texture {texture}")
+        return out
+
     @staticmethod
     def camera(look_at, euler, dist, fovy, aspect):
         out = np.zeros(9, np.float32)
@@ -98,18 +109,23 @@ class Oracle:
         lib().oracle_camera(_fp(la), _fp(eu), float(dist), float(fovy), float(aspect), _fp(out))
         return out
 
-    def render_pixels(self, prm, W, H, xy, look_at=(0, 0, 0), euler=None, dist=3.0, fovy=None):
+    def render_pixels(self, prm, W, H, xy, look_at=(0, 0, 0), euler=None, dist=3.0, fovy=None, with_ub=False):
+        """Colours and intersect() counts of the listed (x, y) pixels; with_ub adds the per-pixel count
+        of shaded hits in the reference's undefined-barycentrics regime."""
         from_rt = _rt()
         euler = from_rt.default_euler() if euler is None else euler
         fovy = from_rt.default_fovy() if fovy is None else fovy
         xy = np.ascontiguousarray(xy, np.int32).reshape(-1, 2)
         rgb = np.zeros(len(xy) * 3, np.float32)
         rays = np.zeros(len(xy), np.uint64)
+        ub = np.zeros(len(xy), np.uint64)
         la = np.asarray(look_at, np.float32)
         eu = np.asarray(euler, np.float32)
         lib().oracle_render_pixels(self.h, _fp(la), _fp(eu), float(dist), float(fovy), W, H, C.addressof(prm),
                                    xy.ctypes.data_as(C.POINTER(C.c_int)), len(xy), _fp(rgb),
-                                   rays.ctypes.data_as(C.POINTER(C.c_uint64)))
+                                   rays.ctypes.data_as(C.POINTER(C.c_uint64)), ub.ctypes.data_as(C.POINTER(C.c_uint64)))
+        if with_ub:
+            return rgb.reshape(-1, 3), rays, ub
         return rgb.reshape(-1, 3), rays
 
     def render(self, prm, W, H, look_at=(0, 0, 0), euler=None, dist=3.0, fovy=None):

@@ -147,21 +147,29 @@ struct Image {
             to_image(iu, iv, 0, x, y);
             return P.texture_filtering == RT_TEX_NEAREST ? nearest(x, y, 0) : bilinear(x, y, 0);
         }
+        // getBestLevelMipmap (:495-529): the floor level is not clamped from above; a level at or
+        // past the chain fails getWidthHeightForLevel (:478-486), so trilinear returns black
+        // (:334-337) and the nearest-level modes white (:270-274, :294-298).  The level is tested
+        // as a float first: (int) of a huge or infinite floor(lod) would be undefined.
         if (P.texture_filtering == RT_TEX_TRILINEAR) {
             if (!mip) return V3(0.0f);
+            const float flo = fmax_g(0.0f, std::floor(lod));
+            if (!(flo < (float)nlevels())) return V3(0.0f);
             const int hi = (int)fmin_g(nlevels() - 1.0f, std::ceil(lod));
-            const int lo = (int)fmax_g(0.0f, std::floor(lod));
+            const int lo = (int)flo;
             float xl, yl, xh, yh;
             to_image(iu, iv, lo, xl, yl);
             to_image(iu, iv, hi, xh, yh);
             return lerp((float)lo, (float)hi, bilinear(xl, yl, lo), bilinear(xh, yh, hi), lod);
         }
         if (!mip) return V3(1.0f);
-        unsigned best;
+        float fbest;
         if (lod - std::floor(lod) < std::ceil(lod) - lod)
-            best = (int)fmax_g(0.0f, std::floor(lod));
+            fbest = fmax_g(0.0f, std::floor(lod));
         else
-            best = (int)fmin_g(nlevels() - 1.0f, std::ceil(lod));
+            fbest = fmin_g(nlevels() - 1.0f, std::ceil(lod));
+        if (!(fbest < (float)nlevels())) return V3(1.0f);
+        const unsigned best = (unsigned)(int)fbest;
         to_image(iu, iv, (int)best, x, y);
         return P.texture_filtering == RT_TEX_MIP_NEAREST ? nearest(x, y, (int)best) : bilinear(x, y, (int)best);
     }
@@ -187,6 +195,7 @@ struct Hit {
     float u = 0, v = 0;
     bool is_triangle = false;
     int prim = -1;
+    bool ub = false;  // barycentricCoordinates returned false for this hit (src/ray_tracing.cpp:281-295)
     Mat& material(std::vector<Mat>& mats) { return is_triangle ? mats[material_index] : sphere_material; }
 };
 struct Light {  // what getPointLights & co. return (src/shadow.h:14-20)
@@ -276,6 +285,10 @@ static bool hit_triangle(const Vert& a, const Vert& b, const Vert& c, Ray& r, Hi
     }
     const V3 bc = barycentric(a.p, b.p, c.p, h.hitPoint);
     const V3 face = h.normal;
+    // the reference's own checks (isZero: |x| < 1e-4 in double, src/ray_tracing.cpp:15-24): off the
+    // plane or a parallelogram area below 1e-4 make barycentricCoordinates return false; the
+    // pointInTriangle check repeats the test that accepted the hit
+    h.ub = !((double)std::fabs(vdot(face, h.hitPoint - a.p)) < 1e-4) || ((double)par_area(a.p, b.p, c.p) < 1e-4);
     h.normal = a.n * bc.x + b.n * bc.y + c.n * bc.z;
     if (vdot(h.normal, face) < 0) h.normal = -h.normal;
     h.u = a.u * bc.x + b.u * bc.y + c.u * bc.z;
@@ -305,6 +318,7 @@ static bool hit_sphere(const Sph& s, Ray& r, Hit& h, int prim) {
     h.sphere_material = s.mat;
     h.is_triangle = false;
     h.prim = prim;
+    h.ub = false;
     return true;
 }
 
@@ -453,6 +467,7 @@ static bool walk_bvh(const Scene& sc, int ni, Ray& r, Hit& h) {
 
 struct Counter {
     uint64_t rays = 0;
+    uint64_t ub = 0;  // shaded hits in the reference's undefined-barycentrics regime
     // glossy lobes: rand() replaced by a Philox-4x32-10 stream, counter (draw, pixel, sample, 0)
     uint32_t pix = 0, sample = 0, draws = 0;
 };
@@ -685,6 +700,7 @@ static float level_of_detail(const Ray& ray, bool camera_ray, const Hit& h, cons
 static V3 final_color(Scene& sc, const rt_params& P, Ray ray, int level, Counter& cnt) {
     Hit h;
     if (!intersect(sc, ray, h, P.use_bvh != 0, cnt)) return V3(0.0f);
+    if (h.is_triangle && h.ub) cnt.ub++;
     V3 color(0.0f);
     const V3 refl = vreflect(vnormalize(ray.direction), vnormalize(h.normal));
     Mat m = h.material(sc.mats);
@@ -976,7 +992,8 @@ int oracle_camera(const float look[3], const float euler[3], float dist, float f
 // Render the listed pixels (x, y pairs in renderRayTracing's y-up convention).  rgb[i] is the
 // colour setPixel(x, y, .) would store; rays[i] the intersect() calls it took.
 int oracle_render_pixels(oracle_scene* o, const float look[3], const float euler[3], float dist, float fovy,
-                         int W, int H, const rt_params* P, const int* xy, int n, float* rgb, uint64_t* rays) {
+                         int W, int H, const rt_params* P, const int* xy, int n, float* rgb, uint64_t* rays,
+                         uint64_t* ub) {
     const Cam cam = make_cam(look, euler, dist, fovy, float(W) / float(H));
 #pragma omp parallel for schedule(dynamic, 4)
     for (int i = 0; i < n; ++i) {
@@ -986,6 +1003,7 @@ int oracle_render_pixels(oracle_scene* o, const float look[3], const float euler
         rgb[i * 3 + 1] = c.y;
         rgb[i * 3 + 2] = c.z;
         if (rays) rays[i] = cnt.rays;
+        if (ub) ub[i] = cnt.ub;
     }
     return 0;
 }
@@ -1008,6 +1026,18 @@ int oracle_render(oracle_scene* o, const float look[3], const float euler[3], fl
         }
     }
     if (total_rays) *total_rays = total;
+    return 0;
+}
+
+// Image::getPixel(texCoord, lod) (src/image.cpp:77-110) of image `tex` for n (u, v, lod) triples.
+int oracle_tex_sample(oracle_scene* o, int tex, const float* uvl, int n, const rt_params* P, float* rgb) {
+    if (tex < 0 || tex >= (int)o->sc.images.size()) return -1;
+    for (int i = 0; i < n; ++i) {
+        const V3 c = o->sc.images[tex].get_pixel(uvl[3 * i], uvl[3 * i + 1], uvl[3 * i + 2], *P);
+        rgb[3 * i] = c.x;
+        rgb[3 * i + 1] = c.y;
+        rgb[3 * i + 2] = c.z;
+    }
     return 0;
 }
 

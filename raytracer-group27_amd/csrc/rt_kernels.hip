@@ -1,18 +1,16 @@
-// rt_kernels.hip -- MI355X (gfx950) megakernel for the reference's per-pixel hot path.
+// rt_kernels.hip -- device arithmetic shared by the MI355X (gfx950) render kernels.
 //
-// One lane = one pixel (one 8x8 pixel tile per 64-lane wave).  Per lane the kernel runs the
-// reference's recursion tree iteratively:
+// The reference's per-pixel hot path, restated exactly where it decides geometry:
 //   renderRayTracing (src/main.cpp:340-400) -> Trackball::generateRay (framework/src/trackball.cpp:87-98)
 //   -> getFinalColor (src/main.cpp:129-301) -> BoundingVolumeHierarchy::intersect (src/bounding_volume_hierarchy.cpp:49-78)
 //   -> light gathering + cansee (src/shadow.cpp:32-321) -> calcColor (src/main.cpp:112-121)
-// Closest-hit queries walk a binned-SAH BVH2 (64-B nodes, both child boxes per node, near-first,
-// short stack in LDS) but every candidate is accepted or rejected with the reference's own
-// arithmetic (plane/edge test, src/ray_tracing.cpp:42-128; sphere quadratic in double,
-// :182-209), and ties in t go to the first object in the reference's visit order, so the hit is
-// the one the reference's brute-force loop (useBVH=false) or its depth-4 BVH walk (useBVH=true,
-// every shadow ray) returns.  useBVH=true additionally requires every box on the candidate's
-// reference leaf path to pass the reference slab test (src/ray_tracing.cpp:213-264), evaluated
-// lazily and cached per ray.
+// Every candidate is accepted or rejected with the reference's own arithmetic (plane/edge test,
+// src/ray_tracing.cpp:42-128; sphere quadratic in double, :182-209), and ties in t go to the first
+// object in the reference's visit order, so the hit is the one the reference's brute-force loop
+// (useBVH=false) or its depth-4 BVH walk (useBVH=true, every shadow ray) returns.  useBVH=true
+// additionally requires every box on the candidate's reference leaf path to pass the reference slab
+// test (src/ray_tracing.cpp:213-264), evaluated lazily and cached per ray.  The schedule (persistent
+// ray-state-machine kernels, quantised BVH8) lives in rt_megakernel.hip.
 //
 // Compiled with -ffp-contract=off (no FMA contraction), IEEE div/sqrt, f32 denormals kept.
 #include <hip/hip_runtime.h>
@@ -51,8 +49,8 @@ struct DSpot {
 };
 
 struct DevScene {
-    const float4* __restrict__ tri;      // [nrec][4] BVH2 leaf order
-    const float4* __restrict__ nodes;    // [nnodes][4]
+    const float4* __restrict__ tri;      // [nrec][4] triangle records, BVH8 leaf order
+    const float4* __restrict__ nodes;    // [nnodes][8] quantised BVH8 nodes (bvh_build.h)
     const float* __restrict__ nrm;       // [ntri][9] scene order (shading normals)
     const float* __restrict__ uv;        // [ntri][6] scene order
     const int* __restrict__ mesh;        // [ntri] scene order
@@ -98,15 +96,10 @@ struct KParams {
     // bands
     int band_rows, band_rank, band_count, n_local_bands;
     float* out;
-    unsigned long long* stats;  // rays, node visits, tri tests, hits
+    unsigned long long* stats;  // rays, node visits, tri tests, hits, ..., UB-regime hits
     int refill;                 // dynamic-fetch kernel: waiting lanes that end a traversal phase
-    int leaf_batch;             // dynamic-fetch kernel: lanes with postponed leaves that start a leaf phase
-    const float* pre_t;         // precomputed primary hits per job (rt_packet.hip), or null
-    const int* pre_rec;
     uint32_t seed_lo, seed_hi;  // glossy sampling: Philox-4x32-10 key (rt_params.rng_seed)
-    unsigned long long* wave_trace;  // developer trace (RT_WAVE_TRACE=1): per wave (start, end, jobs), or null
-    const int* job_order;            // persistent kernels: k-th job handed out is job_order[k] (rt_schedule.hip), or null
-    int* job_cost;                   // persistent kernels (pixels): queries each job took, or null
+    unsigned long long* wave_trace;  // developer wave trace (rt_ctx_set_option RT_OPT_WAVE_TRACE), or null
     int coop;                        // dynamic-fetch kernel: lane-group traversal of the drain's queries
     int coop_max;                    // ... when at most this many queries are left in the wave
     int coop_reserve;                // ... free pool slots kept for depth-first steps
@@ -140,6 +133,7 @@ __host__ __device__ __forceinline__ float u01(uint32_t x) { return (float)(x >> 
 
 struct Cnt {
     uint32_t rays, nodes, tris, hits;
+    uint32_t ub;                   // shaded hits where barycentricCoordinates returns false (counting builds)
     uint32_t wnodes, wtris, wadv;  // wave-level steps (counted by the first active lane): SIMD efficiency
     unsigned long long cyc_a, cyc_b;  // shader clocks per wave in the state machine / in traversal (df kernel)
     unsigned long long cyc_c, cyc_d;  // ... of cyc_a: advancing finished queries / fetching jobs
@@ -210,7 +204,6 @@ struct Best {
 };
 
 #define RT_NO_HIT (-0x7fffffff - 1)
-#define RT_PRE_NONE (-0x7fffffff)  // INT_MIN + 1: no precomputed primary hit (rt_packet.hip); trace it
 
 // Reference triangle test for one record.  Returns true and the reference t when the
 // reference would accept the triangle with ray.t = +inf (order-free part).
@@ -267,140 +260,6 @@ __device__ __forceinline__ v3 safe_inv(v3 d) {
     return v3{1.0f / x, 1.0f / y, 1.0f / z};
 }
 
-// Conservative slab test against an inflated BVH2 child box; returns the entry distance.
-__device__ __forceinline__ bool box_hit(float lx, float ly, float lz, float hx, float hy, float hz, v3 o, v3 inv,
-                                        float tmax, float& tnear) {
-    const float ax = (lx - o.x) * inv.x, bx = (hx - o.x) * inv.x;
-    const float ay = (ly - o.y) * inv.y, by = (hy - o.y) * inv.y;
-    const float az = (lz - o.z) * inv.z, bz = (hz - o.z) * inv.z;
-    const float t0 = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
-    const float t1 = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
-    tnear = t0;
-    return t0 <= t1 && t1 >= 0.0f && t0 <= tmax;
-}
-
-// mode REF: useBVH=true semantics (leaf-path mask + DFS-rank tie-break)
-// ANY: any-hit with threshold `thr` (occluded iff some valid candidate has t <= thr)
-template <bool REF, bool ANY, bool COUNT>
-__device__ bool traverse(const DevScene& S, v3 o, v3 d, v3 nd, float t_init, float thr, Best& best, int* stk,
-                         Cnt& cnt) {
-    best.t = t_init;
-    best.key = -1;  // a candidate tying the caller's initial ray.t is rejected (strict t < ray.t)
-    best.rec = RT_NO_HIT;
-    RefMask mask{0u, 0u};
-    const v3 inv = safe_inv(d);
-    float tcull = ANY ? thr : t_init;
-    int sp = 0;
-    int node = 0;
-    bool found = false;
-    // The reference measures t along normalize(dir) but places the test point at o + dir*t
-    // (src/ray_tracing.cpp:71,111), so for a non-unit direction the accepted point lies off the
-    // triangle and no bounding volume can find it: such rays (only reachable through
-    // rt_intersect / rt_shade; every ray the renderer makes is unit length) test every record.
-    const float dd = dot(d, d);
-    if (!(fabsf(dd - 1.0f) <= 4e-6f)) {
-        for (int r = 0; r < S.ntri; ++r) {
-            const float4* tp = S.tri + r * 4;
-            const float4 r0 = tp[0], r1 = tp[1], r2 = tp[2], r3 = tp[3];
-            if (COUNT) cnt.tris++;
-            float t;
-            if (!tri_test(r0, r1, r2, r3, o, d, nd, t)) continue;
-            const int key = REF ? __float_as_int(r3.z) : __float_as_int(r3.y);
-            if (ANY) {
-                if (!(t <= thr)) continue;
-            } else {
-                if (!(t < best.t || (t == best.t && key < best.key))) continue;
-            }
-            if (REF && !leaf_reachable(S, __float_as_int(r3.w), o, nd, mask)) continue;
-            best.t = t;
-            best.key = key;
-            best.rec = r;
-            found = true;
-            if (ANY) return true;
-        }
-    } else if (S.ntri > 0) {
-        for (;;) {
-            const float4* np = S.nodes + node * 4;
-            const float4 a = np[0];
-            const float4 b = np[1];
-            const float4 c = np[2];
-            const float4 e = np[3];
-            const int c0 = __float_as_int(e.x), c1 = __float_as_int(e.y);
-            const int n0 = __float_as_int(e.z), n1 = __float_as_int(e.w);
-            if (COUNT) cnt.nodes++;
-            float tn0 = 0.0f, tn1 = 0.0f;
-            bool h0 = (c0 >= 0) && box_hit(a.x, a.y, a.z, a.w, b.x, b.y, o, inv, tcull, tn0);
-            bool h1 = (c1 >= 0) && box_hit(b.z, b.w, c.x, c.y, c.z, c.w, o, inv, tcull, tn1);
-            // leaves are tested in place
-#pragma unroll
-            for (int side = 0; side < 2; ++side) {
-                const bool hs = side == 0 ? h0 : h1;
-                const int cnum = side == 0 ? n0 : n1;
-                const int first = side == 0 ? c0 : c1;
-                if (hs && cnum > 0) {
-                    for (int r = first; r < first + cnum; ++r) {
-                        const float4* tp = S.tri + r * 4;
-                        const float4 r0 = tp[0], r1 = tp[1], r2 = tp[2], r3 = tp[3];
-                        if (COUNT) cnt.tris++;
-                        float t;
-                        if (!tri_test(r0, r1, r2, r3, o, d, nd, t)) continue;
-                        const int key = REF ? __float_as_int(r3.z) : __float_as_int(r3.y);
-                        if (ANY) {
-                            if (!(t <= thr)) continue;
-                        } else {
-                            if (!(t < best.t || (t == best.t && key < best.key))) continue;
-                        }
-                        if (REF && !leaf_reachable(S, __float_as_int(r3.w), o, nd, mask)) continue;
-                        best.t = t;
-                        best.key = key;
-                        best.rec = r;
-                        found = true;
-                        if (ANY) return true;
-                        tcull = t;
-                    }
-                    if (side == 0) h0 = false;
-                    else h1 = false;
-                }
-            }
-            h0 = h0 && tn0 <= tcull;
-            h1 = h1 && tn1 <= tcull;
-            if (h0 && h1) {
-                const bool first0 = tn0 <= tn1;
-                stk[sp * RT_WAVE] = first0 ? c1 : c0;
-                ++sp;
-                node = first0 ? c0 : c1;
-            } else if (h0) {
-                node = c0;
-            } else if (h1) {
-                node = c1;
-            } else {
-                if (sp == 0) break;
-                --sp;
-                node = stk[sp * RT_WAVE];
-            }
-        }
-    }
-    // spheres: all tested (few); order handled by key
-    for (int s = 0; s < S.nsph; ++s) {
-        const DSph sp_ = S.sph[s];
-        float t;
-        if (!sphere_test(sp_, o, d, t)) continue;
-        const int key = REF ? sp_.key_bvh : S.ntri + s;
-        if (ANY) {
-            if (!(t <= thr)) continue;
-        } else {
-            if (!(t < best.t || (t == best.t && key < best.key))) continue;
-        }
-        if (REF && !leaf_reachable(S, sp_.leaf, o, nd, mask)) continue;
-        best.t = t;
-        best.key = key;
-        best.rec = -s - 1;
-        found = true;
-        if (ANY) return true;
-    }
-    return found;
-}
-
 // HitInfo for the winner: hitPoint, normal (interpolated + flipped), material, uv.
 struct Surf {
     v3 p;
@@ -410,6 +269,7 @@ struct Surf {
     int mesh;
     int prim;
     bool is_tri;
+    bool ub;  // triangle hit where barycentricCoordinates returns false (src/ray_tracing.cpp:281-295)
 };
 
 // ------------------------------------------------------------------------------------------
@@ -476,17 +336,26 @@ __device__ v3 tex_get_pixel(const DevScene& S, int t, v2 tc, float lod) {
     if (f == RT_TEX_NEAREST) return tex_nearest(S, ti, tex_image_coords(ti, in, 0), 0);
     if (f == RT_TEX_BILINEAR) return tex_bilinear(S, ti, tex_image_coords(ti, in, 0), 0);
     const int nlev = ti.w;
+    // getBestLevelMipmap (:495-529): mode 1 = min(levels - 1, ceil(lod)), mode 2 = max(0, floor(lod)),
+    // mode 0 = the nearer of the two.  The floor level is not clamped from above: at lod >= levels
+    // (+inf included) getWidthHeightForLevel fails (:478-486) and the filter returns its error colour
+    // -- black for trilinear (:334-337), white for the nearest-level modes (:270-274, :294-298).
+    // The level is compared as a float before any int conversion, so a huge lod is never converted.
     if (f == RT_TEX_TRILINEAR) {
         if (nlev == 0) return v3{0.0f, 0.0f, 0.0f};
+        const float flo = gmax(0.0f, floorf(lod));
+        if (!(flo < (float)nlev)) return v3{0.0f, 0.0f, 0.0f};
         const int hi = (int)gmin((float)nlev - 1.0f, ceilf(lod));
-        const int lo = (int)gmax(0.0f, floorf(lod));
+        const int lo = (int)flo;
         const v3 cl = tex_bilinear(S, ti, tex_image_coords(ti, in, lo), lo);
         const v3 ch = tex_bilinear(S, ti, tex_image_coords(ti, in, hi), hi);
         return tex_lerp((float)lo, (float)hi, cl, ch, lod);
     }
     if (nlev == 0) return v3{1.0f, 1.0f, 1.0f};
-    const int best = (lod - floorf(lod) < ceilf(lod) - lod) ? (int)gmax(0.0f, floorf(lod))
-                                                           : (int)gmin((float)nlev - 1.0f, ceilf(lod));
+    const float fbest = (lod - floorf(lod) < ceilf(lod) - lod) ? gmax(0.0f, floorf(lod))
+                                                              : gmin((float)nlev - 1.0f, ceilf(lod));
+    if (!(fbest < (float)nlev)) return v3{1.0f, 1.0f, 1.0f};
+    const int best = (int)fbest;
     const v2 ic = tex_image_coords(ti, in, best);
     return f == RT_TEX_MIP_NEAREST ? tex_nearest(S, ti, ic, best) : tex_bilinear(S, ti, ic, best);
 }
@@ -557,6 +426,11 @@ __device__ __forceinline__ Surf surface(const DevScene& S, v3 o, v3 d, const Bes
             bc.y = length(cross(s.p - v0, v2 - v0)) / A;
             bc.z = length(cross(v1 - v0, s.p - v0)) / A;
         }
+        // the reference's own checks (isZero = |x| < 1e-4 compared in double, :15-24): off the
+        // triangle's plane, or a parallelogram area below 1e-4 -- the pointInTriangle check passes,
+        // it is the test that accepted the hit.  Where they fail the reference interpolates from
+        // uninitialised coordinates (:147-157); the unthresholded ones above are used instead.
+        s.ub = !((double)fabsf(dot(fn, s.p - v0)) < 1e-4) || ((double)A < 1e-4);
         const float* nn = S.nrm + (size_t)sidx * 9;
         const v3 n0{nn[0], nn[1], nn[2]}, n1{nn[3], nn[4], nn[5]}, n2{nn[6], nn[7], nn[8]};
         v3 n = (n0 * bc.x + n1 * bc.y) + n2 * bc.z;
@@ -591,46 +465,9 @@ __device__ __forceinline__ Surf surface(const DevScene& S, v3 o, v3 d, const Bes
         s.mesh = -1;
         s.prim = S.ntri + si;
         s.is_tri = false;
+        s.ub = false;
     }
     return s;
-}
-
-// ------------------------------------------------------------------------------------------
-// cansee (src/shadow.cpp:32-69): loop over transparent occluders with Fresnel attenuation.
-// ------------------------------------------------------------------------------------------
-template <bool COUNT>
-__device__ bool cansee(const DevScene& S, v3 p1, v3 p2, float& intensity, int* stk, Cnt& cnt) {
-    v3 o = p1;
-    v3 d = p2 - p1;
-    float distance = length(d);
-    d = normalize(d);
-    o = o + 0.0005f * d;
-    // d is already normalized; normalize(d) inside the triangle test is recomputed as the
-    // reference does (normalize of a unit vector is not always the identity in float).
-    const v3 nd = normalize(d);
-    while (distance > 0.0005f) {
-        cnt.rays++;
-        const float thr = distance - 2.0f * 0.0005f;
-        Best b;
-        if (S.all_opaque) {
-            // no transparent candidate can exist: occluded iff any valid candidate has t <= thr
-            return !traverse<true, true, COUNT>(S, o, d, nd, FLT_MAX, thr, b, stk, cnt);
-        }
-        const bool hit = traverse<true, false, COUNT>(S, o, d, nd, FLT_MAX, 0.0f, b, stk, cnt);
-        if (!hit || (b.t > thr)) return true;
-        const Surf s = surface(S, o, d, b);
-        if (s.m.transp != 1.0f) {
-            distance -= b.t;
-            o = s.p + 0.0005f * d;
-            const float c = fabsf(dot(d, s.n));
-            const float R0 = s.m.transp;
-            intensity = (float)((double)intensity *
-                                (1.0 - ((double)R0 + (double)(1.0f - R0) * pow((double)(1.0f - c), 5.0))));
-        } else {
-            return false;
-        }
-    }
-    return true;
 }
 
 // calcColor (src/main.cpp:112-121)
@@ -645,223 +482,26 @@ __device__ __forceinline__ v3 calc_color(v3 lcolor, float intensity, float cosL,
 
 __device__ __forceinline__ v3 ld3(const float* p) { return v3{p[0], p[1], p[2]}; }
 
-// Direct light: getPointLights, getSpherelights, getSpotLichts, getPlaneLights (src/shadow.cpp:106-321),
-// summed in that order as getFinalColor does (src/main.cpp:174-185).
-template <bool COUNT>
-__device__ v3 direct_light(const KParams& P, const Surf& s, v3 refl, int* stk, Cnt& cnt) {
-    const DevScene& S = P.S;
-    v3 color{0.0f, 0.0f, 0.0f};
-    const v3 nN = normalize(s.n);
-    const v3 nR = normalize(refl);
-    for (int i = 0; i < S.npl; ++i) {
-        const rt_point_light L = S.pl[i];
-        const v3 lp = ld3(L.position);
-        float intensity = 1.0f;
-        if (cansee<COUNT>(S, s.p, lp, intensity, stk, cnt)) {
-            const v3 ldir = normalize(lp - s.p);
-            const float cosL = fabsf(dot(nN, ldir));
-            const float dd = dot(nR, ldir);
-            const float cosS = (0.0f < dd) ? dd : 0.0f;  // std::max(0.0f, x)
-            color += calc_color(ld3(L.color), intensity, cosL, cosS, s.m);
-        }
-    }
-    for (int i = 0; i < S.nsl; ++i) {
-        const rt_spherical_light L = S.sl[i];
-        const v3 lp = ld3(L.position);
-        float intensity = 1.0f;
-        float intensitySum = 1.0f;
-        int hits = 0;
-        if (cansee<COUNT>(S, s.p, lp, intensitySum, stk, cnt)) hits++;
-        v3 dd = lp - s.p;
-        dd = normalize(dd);
-        v3 notd = dd;
-        if (dd.x != 0.0f) {
-            notd.y = -dd.x;
-            notd.x = dd.y;
-        } else {
-            notd.y = -dd.z;
-            notd.z = dd.y;
-        }
-        v3 perp = normalize(cross(dd, notd)) * L.radius;
-        const m3 rot = rodrigues(P.sl_sin, P.sl_1mcos, dd);
-        const int m = P.sl_m, n = P.sl_n;
-        for (int i2 = 0; i2 < n; ++i2) {
-            for (int j = 0; j < m; ++j) {
-                intensity = 1.0f;
-                if (cansee<COUNT>(S, s.p, lp + ((float)(m - j) / (float)m) * perp, intensity, stk, cnt)) {
-                    hits++;
-                    intensitySum += intensity;
-                }
-            }
-            perp = mul(rot, perp);
-        }
-        if (hits > 0) {
-            const float li = intensitySum / (float)P.sl_count;
-            const v3 ldir = normalize(lp - s.p);
-            const float cosL = fabsf(dot(nN, ldir));
-            const float d2 = dot(nR, ldir);
-            const float cosS = (0.0f < d2) ? d2 : 0.0f;
-            color += calc_color(ld3(L.color), li, cosL, cosS, s.m);
-        }
-    }
-    for (int i = 0; i < S.nspot; ++i) {
-        const DSpot L = S.spot[i];
-        const v3 lp = ld3(L.pos);
-        if (dot(normalize(ld3(L.dir)), normalize(s.p - lp)) > L.cos_angle) {
-            float intensity = 1.0f;
-            if (cansee<COUNT>(S, s.p, lp, intensity, stk, cnt)) {
-                const v3 ldir = normalize(lp - s.p);
-                const float cosL = fabsf(dot(nN, ldir));
-                const float d2 = dot(nR, ldir);
-                const float cosS = (0.0f < d2) ? d2 : 0.0f;
-                color += calc_color(ld3(L.color), intensity, cosL, cosS, s.m);
-            }
-        }
-    }
-    for (int i = 0; i < S.nplane; ++i) {
-        const rt_plane_light L = S.plane[i];
-        const int k = P.plane_k;
-        float hit = 0.0f;
-        int hitCount = 0;
-        float maxCos = 0.0f;
-        float intensitySum = 0.0f;
-        float intensity = 1.0f;
-        const v3 w = ld3(L.width), h = ld3(L.height), lpos = ld3(L.position);
-        const v3 dx = (1.0f / (float)(k - 1)) * w;
-        const v3 dy = (1.0f / (float)(k - 1)) * h;
-        v3 py = lpos;
-        const v3 normal = normalize(cross(w, h));
-        if (dot(normalize(s.p - (lpos + 0.5f * (w + h))), normal) > 0.0f) {
-            for (int i2 = 0; i2 < k; ++i2) {
-                v3 px = py;
-                for (int j = 0; j < k; ++j) {
-                    intensity = 1.0f;
-                    if (cansee<COUNT>(S, s.p, px, intensity, stk, cnt)) {
-                        intensitySum += intensity;
-                        const float dn = dot(normalize(s.p - px), normal);
-                        hit += ((dn < 0.0f) ? 0.0f : dn) / length(s.p - px);
-                        hitCount++;
-                        const float c2 = dot(nR, normalize(px - s.p));
-                        maxCos = (maxCos < c2) ? c2 : maxCos;
-                    }
-                    px = px + dx;
-                }
-                py = py + dy;
-            }
-        }
-        if (hit > 0.0f) {
-            const float li = (intensitySum / (float)hitCount) * hit / (float)(k * k);
-            color += calc_color(ld3(L.color), li, 1.0f, maxCos, s.m);
-        }
-    }
-    return color;
-}
-
 // ------------------------------------------------------------------------------------------
-// getFinalColor as an iterative depth-first walk of its recursion tree.  Each frame keeps the
-// parent's partial colour so children are folded in with the reference's exact nesting:
-//   mirror:      color += (ks * (0 + ks * child)) / glossy_ray_count   (or ks * (...) if shininess == 0)
-//   transparent: color += R * reflectChild;  color += (1-R) * refractChild   (src/main.cpp:191-290)
+// getFinalColor's recursion tree (src/main.cpp:187-290), walked depth first with the colours
+// accumulated forward: a node at weight w adds w * (its direct light) to the sample's colour and
+// hands w * (edge weight) to its children -- ks*ks for a mirror child (ks*ks/N with shininess),
+// R and 1-R for the reflected and refracted rays of a transparent node, ks*max(pow(.)..)/N for a
+// glossy lobe sample.  This is the reference's nested sum reassociated (relative drift ~1e-7,
+// inside the 1e-5 tolerance; the geometry and the ray tree are unchanged).  Only branching nodes
+// leave work behind, so only they push a frame: the pending refracted ray of a transparent node,
+// the lobe of a glossy one (glossy_ray_count > 1).  Pure mirror chains keep no stack.
 // ------------------------------------------------------------------------------------------
-enum { FR_MIRROR = 0, FR_TRANS_A = 1, FR_TRANS_B = 2, FR_GLOSSY = 3 };
+enum { FR_REFRACT = 0, FR_GLOSSY = 1 };
 struct Frame {
-    v3 color;
-    v3 w;      // ks (mirror, glossy) | (reflectionChance, refractionChance, -) (transparent)
-    v3 o2, d2; // pending refracted ray | glossy: reflectColor accumulator, reflect
+    v3 o, d;     // REFRACT: the refracted ray | GLOSSY: hit point, reflect direction
+    v3 w;        // REFRACT: the child's weight | GLOSSY: the node's weight * ks / glossy_ray_count
+    v3 nraw;     // GLOSSY: hitInfo.normal (unnormalised, the lobe's side test)
+    float shin, gd;  // GLOSSY: shininess and the lobe half-width d (host-evaluated per material)
     int mode;
-    int flag;  // mirror: shininess != 0 ; transparent: refracted ray traced ; glossy: sample index
-    // glossy lobe (src/main.cpp:204-250): hit point, hitInfo.normal (unnormalised), current sample
-    // direction, shininess and the lobe half-width d (host-evaluated per material)
-    v3 hp, nraw, sdir;
-    float shin, gd;
-    v3 kd;  // persistent kernels: kd of the shading point at this level (texture or material)
+    int level;   // recursion level of the child rays
+    int sample;  // GLOSSY: lobe samples drawn so far (1 .. glossy_ray_count - 1)
 };
-
-template <bool COUNT>
-__device__ v3 get_final_color(const KParams& P, v3 o, v3 d, float t_init, int* stk, Cnt& cnt) {
-    const DevScene& S = P.S;
-    Frame fr[RT_MAX_DEPTH];
-    int level = 0;
-    for (;;) {
-        v3 col{0.0f, 0.0f, 0.0f};
-        bool descend = false;
-        cnt.rays++;
-        Best b;
-        const v3 nd = normalize(d);
-        bool hit = P.use_bvh ? traverse<true, false, COUNT>(S, o, d, nd, t_init, 0.0f, b, stk, cnt)
-                             : traverse<false, false, COUNT>(S, o, d, nd, t_init, 0.0f, b, stk, cnt);
-        t_init = FLT_MAX;
-        if (hit) {
-            if (COUNT) cnt.hits++;
-            const Surf s = surface(S, o, d, b, true, level == 0);
-            const v3 refl = reflect(normalize(d), normalize(s.n));
-            col = direct_light<COUNT>(P, s, refl, stk, cnt);
-            if (level < P.max_level) {
-                if (s.m.transp == 1.0f) {
-                    if (s.m.ks[0] > 0.0f || s.m.ks[1] > 0.0f || s.m.ks[2] > 0.0f) {
-                        Frame& f = fr[level];
-                        f.color = col;
-                        f.w = v3{s.m.ks[0], s.m.ks[1], s.m.ks[2]};
-                        f.mode = FR_MIRROR;
-                        f.flag = (s.m.shin != 0.0f);
-                        o = s.p + 0.01f * refl;
-                        d = refl;
-                        descend = true;
-                    }
-                } else {
-                    const v3 l = normalize(d);
-                    const v3 n = normalize(s.n);
-                    const float r = P.refr;
-                    const float c = fabsf(dot(l, n));
-                    v3 refr = r * l + (r * c - sqrtf(1.0f - r * r * (1.0f - c * c))) * n;
-                    refr = normalize(refr);
-                    const float R0 = s.m.transp;
-                    const float reflC = (float)((double)R0 + (double)(1.0f - R0) * pow((double)(1.0f - c), 5.0));
-                    const float refrC = 1.0f - reflC;
-                    Frame& f = fr[level];
-                    f.color = col;
-                    f.w = v3{reflC, refrC, 0.0f};
-                    f.o2 = s.p + 0.01f * refr;
-                    f.d2 = refr;
-                    f.mode = FR_TRANS_A;
-                    f.flag = (r * r * (1.0f - c * c) <= 1.0f);
-                    o = s.p + 0.01f * refl;
-                    d = refl;
-                    descend = true;
-                }
-            }
-        }
-        if (descend) {
-            ++level;
-            continue;
-        }
-        v3 child = col;
-        bool resumed = false;
-        while (level > 0) {
-            --level;
-            Frame& f = fr[level];
-            if (f.mode == FR_MIRROR) {
-                const v3 rc = v3{0.0f, 0.0f, 0.0f} + f.w * child;
-                const v3 add = f.flag ? (f.w * rc) / (float)P.glossy_n : f.w * rc;
-                child = f.color + add;
-            } else if (f.mode == FR_TRANS_A) {
-                f.color = f.color + f.w.x * child;
-                if (f.flag) {
-                    f.mode = FR_TRANS_B;
-                    o = f.o2;
-                    d = f.d2;
-                    ++level;
-                    resumed = true;
-                    break;
-                }
-                child = f.color;
-            } else {
-                child = f.color + f.w.y * child;
-            }
-        }
-        if (!resumed) return child;
-    }
-}
 
 __device__ __forceinline__ void gen_ray(const KParams& P, float px, float py, v3& o, v3& d) {
     const v3 csd = normalize(v3{-px * P.hw, py * P.hh, 1.0f});
@@ -912,119 +552,11 @@ __device__ void flush_counters(const KParams& P, const Cnt& c) {
             atomicAdd(P.stats + 11, c.cyc_d);
         }
     }
-}
-
-// One 64-lane block renders one 8x8 pixel tile of one band.
-template <bool COUNT>
-__global__ __launch_bounds__(64) void render_kernel(KParams P) {
-    __shared__ int stack_lds[RT_STACK_SIZE * RT_WAVE];
-    const int lane = threadIdx.x;
-    int* stk = stack_lds + lane;
-    const int tiles_x = (P.W + 7) / 8;
-    const int tiles_y_band = (P.band_rows + 7) / 8;
-    const int tile = blockIdx.x;
-    const int tx = tile % tiles_x;
-    const int rest = tile / tiles_x;
-    const int ty = rest % tiles_y_band;
-    const int lb = rest / tiles_y_band;  // local band
-    const int gb = lb * P.band_count + P.band_rank;
-    const int row_in_band = ty * 8 + (lane >> 3);
-    const int x = tx * 8 + (lane & 7);
-    const int y = gb * P.band_rows + row_in_band;
-    Cnt cnt{0u, 0u, 0u, 0u};
-    const bool active = (x < P.W) && (row_in_band < P.band_rows) && (y < P.H) && (lb < P.n_local_bands);
-    if (active) {
-        const float ndx = (float)x / (float)P.W * 2.0f - 1.0f;
-        const float ndy = (float)y / (float)P.H * 2.0f - 1.0f;
-        v3 col;
-        v3 o, d;
-        if (P.aa) {
-            const float sx[4] = {ndx - P.aa_offx, ndx + P.aa_offx, ndx - P.aa_offx, ndx + P.aa_offx};
-            const float sy[4] = {ndy + P.aa_offy, ndy + P.aa_offy, ndy - P.aa_offy, ndy - P.aa_offy};
-            v3 acc{0.0f, 0.0f, 0.0f};
-            for (int i = 0; i < 4; ++i) {
-                gen_ray(P, sx[i], sy[i], o, d);
-                acc += get_final_color<COUNT>(P, o, d, FLT_MAX, stk, cnt);
-            }
-            col = acc * 0.25f;
-        } else if (P.multi) {
-            const float qs[4][2] = {{-1.0f, 1.0f}, {1.0f, 1.0f}, {-1.0f, -1.0f}, {1.0f, -1.0f}};
-            v3 acc{0.0f, 0.0f, 0.0f};
-            for (int i = 0; i < 4; ++i)
-                for (int xx = 1; xx <= P.ms_moves; xx += 2)
-                    for (int yy = 1; yy <= P.ms_moves; yy += 2) {
-                        const float rx = ndx + (P.ms_offx * qs[i][0] * (float)xx);
-                        const float ry = ndy + (P.ms_offy * qs[i][1] * (float)yy);
-                        gen_ray(P, rx, ry, o, d);
-                        acc += get_final_color<COUNT>(P, o, d, FLT_MAX, stk, cnt);
-                    }
-            col = acc * (float)(1.0f / (float)P.sample_size);
-        } else {
-            gen_ray(P, ndx, ndy, o, d);
-            col = get_final_color<COUNT>(P, o, d, FLT_MAX, stk, cnt);
-        }
-        float* dst = P.out + (((size_t)lb * P.band_rows + row_in_band) * P.W + x) * 3;
-        dst[0] = col.x;
-        dst[1] = col.y;
-        dst[2] = col.z;
+    if (COUNT) {
+        unsigned long long u = c.ub;
+        for (int off = 32; off > 0; off >>= 1) u += __shfl_xor(u, off);
+        if ((threadIdx.x & 63) == 0) atomicAdd(P.stats + 12, u);
     }
-    flush_counters<COUNT>(P, cnt);
-}
-
-// Per-ray kernels for rt_intersect / rt_shade.
-__global__ __launch_bounds__(64) void intersect_kernel(KParams P, const rt_ray* rays, int n, int use_bvh, rt_hit* hits) {
-    __shared__ int stack_lds[RT_STACK_SIZE * RT_WAVE];
-    const int i = blockIdx.x * 64 + threadIdx.x;
-    int* stk = stack_lds + threadIdx.x;
-    if (i >= n) return;
-    const rt_ray r = rays[i];
-    const v3 o{r.origin[0], r.origin[1], r.origin[2]};
-    const v3 d{r.direction[0], r.direction[1], r.direction[2]};
-    const v3 nd = normalize(d);
-    Best b;
-    Cnt cnt{0u, 0u, 0u, 0u};
-    const bool hit = use_bvh ? traverse<true, false, false>(P.S, o, d, nd, r.t, 0.0f, b, stk, cnt)
-                             : traverse<false, false, false>(P.S, o, d, nd, r.t, 0.0f, b, stk, cnt);
-    rt_hit h;
-    h.hit = hit ? 1 : 0;
-    h.t = hit ? b.t : r.t;
-    if (hit) {
-        const Surf s = surface(P.S, o, d, b);
-        h.normal[0] = s.n.x;
-        h.normal[1] = s.n.y;
-        h.normal[2] = s.n.z;
-        h.hit_point[0] = s.p.x;
-        h.hit_point[1] = s.p.y;
-        h.hit_point[2] = s.p.z;
-        h.uv[0] = s.uv.x;
-        h.uv[1] = s.uv.y;
-        h.material_index = s.mesh;
-        h.prim_id = s.prim;
-        h.is_triangle = s.is_tri ? 1 : 0;
-    } else {
-        for (int k = 0; k < 3; ++k) h.normal[k] = h.hit_point[k] = 0.0f;
-        h.uv[0] = h.uv[1] = 0.0f;
-        h.material_index = -1;
-        h.prim_id = -1;
-        h.is_triangle = 0;
-    }
-    hits[i] = h;
-}
-
-__global__ __launch_bounds__(64) void shade_kernel(KParams P, const rt_ray* rays, int n, float* rgb,
-                                                   unsigned long long* ray_counts) {
-    __shared__ int stack_lds[RT_STACK_SIZE * RT_WAVE];
-    const int i = blockIdx.x * 64 + threadIdx.x;
-    int* stk = stack_lds + threadIdx.x;
-    if (i >= n) return;
-    const rt_ray r = rays[i];
-    Cnt cnt{0u, 0u, 0u, 0u};
-    const v3 c = get_final_color<false>(P, v3{r.origin[0], r.origin[1], r.origin[2]},
-                                        v3{r.direction[0], r.direction[1], r.direction[2]}, r.t, stk, cnt);
-    rgb[i * 3 + 0] = c.x;
-    rgb[i * 3 + 1] = c.y;
-    rgb[i * 3 + 2] = c.z;
-    ray_counts[i] = cnt.rays;
 }
 
 // Gathered band buffers [band_count][max_local][band_rows][W][3] -> setPixel layout
@@ -1045,6 +577,38 @@ __global__ void unpermute_kernel(int W, int H, int band_rows, int band_count, in
     d[0] = s[0];
     d[1] = s[1];
     d[2] = s[2];
+}
+
+// Image::getPixel(uv, lod) on texture `t` for n (u, v, lod) triples (rt_texture_sample).
+// A view batch gathered from band_count ranks, [band_count][n_views][max_local][band_rows][W][3] (each
+// rank's rt_render_views_device buffer back to back), -> n_views images in the setPixel layout.
+__global__ void unpermute_views_kernel(int W, int H, int band_rows, int band_count, int max_local, int n_views,
+                                       const float* src, float* dst) {
+    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t per_view = (size_t)W * H;
+    if (idx >= per_view * n_views) return;
+    const int v = (int)(idx / per_view);
+    const size_t pix = idx - (size_t)v * per_view;
+    const int x = (int)(pix % W);
+    const int y = (int)(pix / W);
+    const int gb = y / band_rows;
+    const int r = y % band_rows;
+    const int rank = gb % band_count;
+    const int lb = gb / band_count;
+    const float* s = src + (((((size_t)rank * n_views + v) * max_local + lb) * band_rows + r) * W + x) * 3;
+    float* d = dst + ((size_t)v * per_view + (size_t)(H - 1 - y) * W + x) * 3;
+    d[0] = s[0];
+    d[1] = s[1];
+    d[2] = s[2];
+}
+
+__global__ void tex_sample_kernel(DevScene S, int t, const float* uvl, int n, float* out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const v3 c = tex_get_pixel(S, t, v2{uvl[3 * i], uvl[3 * i + 1]}, uvl[3 * i + 2]);
+    out[3 * i] = c.x;
+    out[3 * i + 1] = c.y;
+    out[3 * i + 2] = c.z;
 }
 
 __global__ void selftest_kernel(const float* x, const float* y, int n, float* out) {

@@ -1,51 +1,56 @@
-// rt_megakernel.hip -- persistent ray-state-machine megakernel (included by rt_runtime.hip after
-// rt_kernels.hip, whose device helpers it reuses).
+// rt_megakernel.hip -- persistent ray-state-machine render kernels (included by rt_runtime.hip after
+// rt_kernels.hip, whose device helpers they use).
 //
 // Why: the recursive reference (getFinalColor -> lights -> cansee -> intersect) compiled as nested
-// inlined calls gives ~5 traversal instances, 256 VGPRs and one wave per SIMD, and a wave is held
-// by its slowest pixel.  Here every lane is a small state machine whose only expensive step is
-// ONE shared traversal: in each iteration every busy lane traces whatever query its state needs
-// (camera ray, mirror/refracted ray, or a shadow segment), then advances its state until it needs
-// the next query.  A lane that finishes its pixel takes the next one from a global counter
-// (wave-aggregated atomic), so no lane idles while work remains.
+// inlined calls holds several traversal instances live at once and a wave is held by its slowest
+// pixel.  Here every lane is a small state machine whose only expensive step is ONE shared
+// traversal: each lane traces whatever query its state needs (camera ray, mirror / reflected /
+// refracted / glossy ray, or one cansee segment), then advances its state until it needs the next
+// query.  A lane that finishes its pixel takes the next one from a job counter (wave-aggregated
+// atomic), so no lane idles while work remains.
 //
-// The arithmetic of every step is exactly the reference's (same helpers as rt_kernels.hip); only
-// the schedule differs.  Reference map: pixel/sample loop src/main.cpp:344-395, getFinalColor
-// :129-301, lights src/shadow.cpp:106-321, cansee src/shadow.cpp:32-69.
+// The arithmetic of every step is the reference's (rt_kernels.hip helpers); only the schedule
+// differs.  Reference map: pixel/sample loop src/main.cpp:344-395, getFinalColor :129-301, lights
+// src/shadow.cpp:106-321, cansee src/shadow.cpp:32-69.  Two kernels share the state machine:
+//   persistent_kernel     whole-traversal refill (scenes < 65 536 triangles: a query is a handful of
+//                         node visits and per-step bookkeeping does not pay)
+//   persistent_df_kernel  dynamic fetch: the traversal is resumable and advanced one node visit or
+//                         one triangle record per iteration; lanes whose query completes park until
+//                         enough of the wave waits, then the wave advances them together.
 
 namespace rt {
 
-enum QType { Q_PATH = 0, Q_SHADOW = 1 };
 enum LType { L_POINT = 0, L_SPHERE = 1, L_SPOT = 2, L_PLANE = 3, L_DONE = 4 };
 
+// The query a lane traces next: a getFinalColor ray or one cansee segment (Lane::shadow).
+struct Query {
+    v3 o, d;
+    float t;  // initial ray.t: FLT_MAX, or the caller's ray.t for rt_shade's explicit rays
+};
+
+// Per-lane state between queries: the pixel, the position in the recursion tree and in the light
+// loop of the current shading point.  Kept small: it is live across every traversal step.
 struct Lane {
-    // job
-    int job;     // -1: idle
-    int sample;  // sub-sample index (AA / getPixelRays)
-    int nsamples;
-    int px, py, out_row;  // pixel, row inside the local band buffer
-    v3 pacc;
-    // query
-    v3 qo, qd;
-    float qt;  // initial ray.t
-    int qtype;
-    // path
-    int level;
-    v3 cur_d;  // direction of the ray that produced the current shading point
-    // shading point
-    v3 hp, nN, nR, refl;
-    int mat;  // >= 0 mesh material, < 0: sphere -(s+1)
-    v3 color;
-    // light loop
-    int lt, li, ls;
+    int job;        // >= 0 job index; -1 idle (fetch another); -2 no more work
+    uint32_t rpix;  // the reference's pixel id y * W + x (rt_shade: the ray index), glossy Philox counter
+    int out_row;    // row of the pixel in the band buffer
+    int sample;     // camera sample (AA / getPixelRays)
+    int level;      // recursion level of the current node
+    int nfr;        // pending frames (transparent / glossy branches)
+    bool desc;      // the current node descends to its mirror / reflected child after its lights
+    bool shadow;    // the query in flight is a cansee segment
+    v3 pacc;        // pixel: sum of the finished camera samples
+    v3 acc;         // current camera sample: forward-accumulated colour
+    v3 w, wc;       // weight of the current node / of its mirror or reflected child
+    v3 hp, nN, nR, refl;  // shading point: hitPoint, normalize(normal), normalize(reflect), reflect
+    int mat;        // >= 0 mesh material, < 0: sphere -(s+1)
+    v3 color;       // direct light of the current node
+    int lt, li, ls; // light loop: type, index, sample
     float a0, a1, a2, a3;  // per-light accumulators
-    v3 u0, u1;             // perp | (px, py)
-    // cansee
-    v3 so, sd;
-    float sdist, sI;
-    // glossy lobes: hitInfo.normal of the shading point, Philox draw counter and pixel id
-    v3 nraw;
-    uint32_t draws, rpix;
+    v3 u0, u1;             // spherical light: perp | plane light: (px, py)
+    float sdist, sI;       // cansee: remaining distance, intensity
+    uint32_t draws;        // glossy: Philox draws of this camera sample
+    v3 kd;                 // TEX kernels: kd of the shading point (texture or material)
 };
 
 __device__ __forceinline__ DMat load_mat(const DevScene& S, int m) {
@@ -53,150 +58,17 @@ __device__ __forceinline__ DMat load_mat(const DevScene& S, int m) {
     return S.sph[-m - 1].m;
 }
 
-// matForRendering (src/main.cpp:146-171): the shading point's material with its kd, which
-// surface() took from the texture when there is one; kept in the level's frame (scratch), not
-// in the lane's registers
+// matForRendering (src/main.cpp:146-171): the shading point's material with the kd surface() took
+// from its texture, if any
 template <bool TEX>
-__device__ __forceinline__ DMat render_mat(const DevScene& S, const Lane& L, const Frame* fr) {
+__device__ __forceinline__ DMat render_mat(const DevScene& S, const Lane& L) {
     DMat m = load_mat(S, L.mat);
-    if (!TEX) return m;
-    const v3 kd = fr[L.level].kd;
-    m.kd[0] = kd.x;
-    m.kd[1] = kd.y;
-    m.kd[2] = kd.z;
+    if (TEX) {
+        m.kd[0] = L.kd.x;
+        m.kd[1] = L.kd.y;
+        m.kd[2] = L.kd.z;
+    }
     return m;
-}
-
-// Traversal with run-time mode flags: one instance serves every query type.
-template <bool COUNT>
-__device__ __forceinline__ bool trace_query(const DevScene& S, v3 o, v3 d, float t_init, float thr, bool REF, bool ANY,
-                                            Best& best, int* stk, Cnt& cnt) {
-    const v3 nd = normalize(d);
-    best.t = t_init;
-    best.key = -1;
-    best.rec = RT_NO_HIT;
-    RefMask mask{0u, 0u};
-    float tcull = ANY ? thr : t_init;
-    bool found = false;
-    const float dd = dot(d, d);
-    const bool unit = fabsf(dd - 1.0f) <= 4e-6f;
-    const v3 inv = safe_inv(d);
-    int sp = 0;
-    int node = 0;
-    // non-unit directions: exhaustive (see traverse() in rt_kernels.hip); unit: BVH2
-    int brute_r = 0;
-    const int brute_n = unit ? 0 : S.ntri;
-    bool done = (S.ntri == 0);
-    while (!done) {
-        int first = 0, count = 0;
-        if (!unit) {
-            first = brute_r;
-            count = min(64, brute_n - brute_r);
-            brute_r += count;
-            done = brute_r >= brute_n;
-        } else {
-            const float4* np = S.nodes + node * 4;
-            const float4 a = np[0];
-            const float4 b = np[1];
-            const float4 c = np[2];
-            const float4 e = np[3];
-            const int c0 = __float_as_int(e.x), c1 = __float_as_int(e.y);
-            const int n0 = __float_as_int(e.z), n1 = __float_as_int(e.w);
-            if (COUNT) {
-                cnt.nodes++;
-                if (wave_leader()) cnt.wnodes++;
-            }
-            float tn0 = 0.0f, tn1 = 0.0f;
-            bool h0 = (c0 >= 0) && box_hit(a.x, a.y, a.z, a.w, b.x, b.y, o, inv, tcull, tn0);
-            bool h1 = (c1 >= 0) && box_hit(b.z, b.w, c.x, c.y, c.z, c.w, o, inv, tcull, tn1);
-            const bool l0 = h0 && n0 > 0, l1 = h1 && n1 > 0;
-            h0 = h0 && n0 == 0;
-            h1 = h1 && n1 == 0;
-            // at most two leaf ranges per node: test them below, then descend
-            if (l0 && l1) {
-                // adjacent ranges are not guaranteed; test both in turn
-                for (int r = c0; r < c0 + n0; ++r) {
-                    const float4* tp = S.tri + r * 4;
-                    const float4 r0 = tp[0], r1 = tp[1], r2 = tp[2], r3 = tp[3];
-                    if (COUNT) {
-            cnt.tris++;
-            if (wave_leader()) cnt.wtris++;
-        }
-                    float t;
-                    if (!tri_test(r0, r1, r2, r3, o, d, nd, t)) continue;
-                    const int key = REF ? __float_as_int(r3.z) : __float_as_int(r3.y);
-                    if (ANY ? !(t <= thr) : !(t < best.t || (t == best.t && key < best.key))) continue;
-                    if (REF && !leaf_reachable(S, __float_as_int(r3.w), o, nd, mask)) continue;
-                    best.t = t;
-                    best.key = key;
-                    best.rec = r;
-                    found = true;
-                    if (!ANY) tcull = t;
-                }
-                if (ANY && found) break;
-                first = c1;
-                count = n1;
-            } else if (l0) {
-                first = c0;
-                count = n0;
-            } else if (l1) {
-                first = c1;
-                count = n1;
-            }
-            h0 = h0 && tn0 <= tcull;
-            h1 = h1 && tn1 <= tcull;
-            if (h0 && h1) {
-                const bool near0 = tn0 <= tn1;
-                stk[sp * RT_WAVE] = near0 ? c1 : c0;
-                ++sp;
-                node = near0 ? c0 : c1;
-            } else if (h0) {
-                node = c0;
-            } else if (h1) {
-                node = c1;
-            } else if (sp == 0) {
-                done = true;
-            } else {
-                --sp;
-                node = stk[sp * RT_WAVE];
-            }
-        }
-        for (int r = first; r < first + count; ++r) {
-            const float4* tp = S.tri + r * 4;
-            const float4 r0 = tp[0], r1 = tp[1], r2 = tp[2], r3 = tp[3];
-            if (COUNT) {
-            cnt.tris++;
-            if (wave_leader()) cnt.wtris++;
-        }
-            float t;
-            if (!tri_test(r0, r1, r2, r3, o, d, nd, t)) continue;
-            const int key = REF ? __float_as_int(r3.z) : __float_as_int(r3.y);
-            if (ANY ? !(t <= thr) : !(t < best.t || (t == best.t && key < best.key))) continue;
-            if (REF && !leaf_reachable(S, __float_as_int(r3.w), o, nd, mask)) continue;
-            best.t = t;
-            best.key = key;
-            best.rec = r;
-            found = true;
-            if (!ANY) tcull = t;
-        }
-        if (ANY && found) break;
-    }
-    if (!(ANY && found)) {
-        for (int s = 0; s < S.nsph; ++s) {
-            const DSph sp_ = S.sph[s];
-            float t;
-            if (!sphere_test(sp_, o, d, t)) continue;
-            const int key = REF ? sp_.key_bvh : S.ntri + s;
-            if (ANY ? !(t <= thr) : !(t < best.t || (t == best.t && key < best.key))) continue;
-            if (REF && !leaf_reachable(S, sp_.leaf, o, nd, mask)) continue;
-            best.t = t;
-            best.key = key;
-            best.rec = -s - 1;
-            found = true;
-            if (ANY) break;
-        }
-    }
-    return found;
 }
 
 // 8-wide traversal over the quantised BVH8 (bvh_build.h).  The stack holds node groups
@@ -360,20 +232,18 @@ __device__ __forceinline__ bool trace_query8(const DevScene& S, v3 o, v3 d, floa
 }
 
 // ---- light loop -----------------------------------------------------------------------------
-// Starts cansee(hp, target) (src/shadow.cpp:32-40).  Returns true if a shadow query is needed;
-// otherwise the loop condition `distance > SHADOW_ERROR_OFFSET` failed and cansee returns true.
-__device__ __forceinline__ bool start_cansee(Lane& L, v3 target) {
+// cansee(hp, target) (src/shadow.cpp:32-40): queues the first segment, or returns false when the
+// loop condition distance > SHADOW_ERROR_OFFSET fails at once (cansee returns true, no intersect).
+__device__ __forceinline__ bool start_cansee(Lane& L, v3 target, Query& q) {
     v3 d = target - L.hp;
     L.sdist = length(d);
     d = normalize(d);
-    L.so = L.hp + 0.0005f * d;
-    L.sd = d;
     L.sI = 1.0f;
     if (L.sdist > 0.0005f) {
-        L.qo = L.so;
-        L.qd = L.sd;
-        L.qt = FLT_MAX;
-        L.qtype = Q_SHADOW;
+        q.o = L.hp + 0.0005f * d;
+        q.d = d;
+        q.t = FLT_MAX;
+        L.shadow = true;
         return true;
     }
     return false;
@@ -386,8 +256,7 @@ __device__ __forceinline__ void light_cos(const Lane& L, v3 lp, float& cosL, flo
     cosS = (0.0f < d2) ? d2 : 0.0f;
 }
 
-// Sample target of the current light sample; false when the current light is finished (or
-// skipped) and the caller must move on.
+// getSpherelights' first perp (src/shadow.cpp:160-175)
 __device__ __forceinline__ v3 sphere_perp(const Lane& L, v3 lp, float radius) {
     v3 dd = normalize(lp - L.hp);
     v3 notd = dd;
@@ -401,10 +270,12 @@ __device__ __forceinline__ v3 sphere_perp(const Lane& L, v3 lp, float radius) {
     return normalize(cross(dd, notd)) * radius;
 }
 
-// Advance the light loop until a shadow query is needed (true) or all lights are done (false).
-// `vis` carries the result of the cansee that just finished (valid when have_result).
+// Advance the light loop (getPointLights, getSpherelights, getSpotLichts, getPlaneLights in the
+// order getFinalColor sums them, src/main.cpp:174-185) until a shadow query is needed (true, query
+// in q) or every light is done (false).  `vis` is the result of the cansee that just finished
+// (valid when have_result).
 template <bool TEX>
-__device__ bool advance_lights(const KParams& P, Lane& L, const Frame* fr, bool have_result, bool vis) {
+__device__ bool advance_lights(const KParams& P, Lane& L, bool have_result, bool vis, Query& q) {
     const DevScene& S = P.S;
     for (;;) {
         if (L.lt == L_POINT) {
@@ -414,7 +285,7 @@ __device__ bool advance_lights(const KParams& P, Lane& L, const Frame* fr, bool 
                     const rt_point_light pl = S.pl[L.li];
                     float cosL, cosS;
                     light_cos(L, ld3(pl.position), cosL, cosS);
-                    L.color += calc_color(ld3(pl.color), L.sI, cosL, cosS, render_mat<TEX>(S, L, fr));
+                    L.color += calc_color(ld3(pl.color), L.sI, cosL, cosS, render_mat<TEX>(S, L));
                 }
                 L.li++;
             }
@@ -424,7 +295,7 @@ __device__ bool advance_lights(const KParams& P, Lane& L, const Frame* fr, bool 
                 L.ls = -1;
                 continue;
             }
-            if (start_cansee(L, ld3(S.pl[L.li].position))) return true;
+            if (start_cansee(L, ld3(S.pl[L.li].position), q)) return true;
             have_result = true;
             vis = true;
             continue;
@@ -461,7 +332,7 @@ __device__ bool advance_lights(const KParams& P, Lane& L, const Frame* fr, bool 
                 if (L.a1 > 0.0f) {
                     float cosL, cosS;
                     light_cos(L, lp, cosL, cosS);
-                    L.color += calc_color(ld3(sl.color), L.a0 / (float)P.sl_count, cosL, cosS, render_mat<TEX>(S, L, fr));
+                    L.color += calc_color(ld3(sl.color), L.a0 / (float)P.sl_count, cosL, cosS, render_mat<TEX>(S, L));
                 }
                 L.li++;
                 L.ls = -1;
@@ -473,7 +344,7 @@ __device__ bool advance_lights(const KParams& P, Lane& L, const Frame* fr, bool 
                 const int j = L.ls % m;
                 target = lp + ((float)(m - j) / (float)m) * L.u0;
             }
-            if (start_cansee(L, target)) return true;
+            if (start_cansee(L, target, q)) return true;
             have_result = true;
             vis = true;
             continue;
@@ -485,7 +356,7 @@ __device__ bool advance_lights(const KParams& P, Lane& L, const Frame* fr, bool 
                     const DSpot sp = S.spot[L.li];
                     float cosL, cosS;
                     light_cos(L, ld3(sp.pos), cosL, cosS);
-                    L.color += calc_color(ld3(sp.color), L.sI, cosL, cosS, render_mat<TEX>(S, L, fr));
+                    L.color += calc_color(ld3(sp.color), L.sI, cosL, cosS, render_mat<TEX>(S, L));
                 }
                 L.li++;
             }
@@ -501,7 +372,7 @@ __device__ bool advance_lights(const KParams& P, Lane& L, const Frame* fr, bool 
                 L.li++;
                 continue;
             }
-            if (start_cansee(L, lp)) return true;
+            if (start_cansee(L, lp, q)) return true;
             have_result = true;
             vis = true;
             continue;
@@ -552,13 +423,13 @@ __device__ bool advance_lights(const KParams& P, Lane& L, const Frame* fr, bool 
             if (L.ls >= k * k) {
                 if (L.a0 > 0.0f) {
                     const float li = (L.a3 / (float)(int)L.a1) * L.a0 / (float)(k * k);
-                    L.color += calc_color(ld3(pl.color), li, 1.0f, L.a2, render_mat<TEX>(S, L, fr));
+                    L.color += calc_color(ld3(pl.color), li, 1.0f, L.a2, render_mat<TEX>(S, L));
                 }
                 L.li++;
                 L.ls = -1;
                 continue;
             }
-            if (start_cansee(L, L.u0)) return true;
+            if (start_cansee(L, L.u0, q)) return true;
             have_result = true;
             vis = true;
             continue;
@@ -567,13 +438,14 @@ __device__ bool advance_lights(const KParams& P, Lane& L, const Frame* fr, bool 
     }
 }
 
-// ---- glossy lobe ---------------------------------------------------------------------------
+// ---- recursion tree ------------------------------------------------------------------------
 // Next lobe sample of the glossy frame f (src/main.cpp:209-249): two uniforms per draw from the
 // Philox stream (key = rng_seed, counter = (draw, pixel, sample, 0)) in place of rand(); up to
-// glossy_ray_count / 4 redraws while the direction points into the surface.  Returns true with
-// the sample ray queued; false when the lobe is done.
-__device__ bool glossy_next(const KParams& P, Lane& L, Frame& f) {
-    const v3 r = f.d2;
+// glossy_ray_count / 4 redraws while the direction points into the surface.  Returns true with the
+// sample ray in q and its lobe weight max(pow(dot(reflect, dir), shininess), 0) in cw; false when
+// the lobe is done.
+__device__ bool glossy_next(const KParams& P, Lane& L, Frame& f, Query& q, float& cw) {
+    const v3 r = f.d;
     v3 notr = r;
     if (r.x != 0.0f) {
         notr.y = -r.x;
@@ -584,7 +456,7 @@ __device__ bool glossy_next(const KParams& P, Lane& L, Frame& f) {
     }
     const v3 pr1 = cross(r, notr);
     const v3 pr2 = cross(r, pr1);
-    while (++f.flag < P.glossy_n) {
+    while (++f.sample < P.glossy_n) {
         v3 sd;
         int loops = 0;
         do {
@@ -601,112 +473,110 @@ __device__ bool glossy_next(const KParams& P, Lane& L, Frame& f) {
             loops++;
         } while (dot(sd, f.nraw) <= 0.0f && loops < P.glossy_n / 4);
         if (dot(sd, f.nraw) > 0.0f) {
-            f.sdir = sd;
-            L.qo = f.hp + 0.01f * sd;
-            L.qd = sd;
-            L.qt = FLT_MAX;
-            L.qtype = Q_PATH;
+            q.o = f.o + 0.01f * sd;
+            q.d = sd;
+            q.t = FLT_MAX;
+            cw = gmax(powf(dot(r, sd), f.shin), 0.0f);
             return true;
         }
     }
     return false;
 }
 
-// ---- recursion tree ------------------------------------------------------------------------
-// After the direct light of the shading point at L.level: descend (returns true with the
-// child ray queued) or fold the finished subtree into its ancestors.  Returns false when the
-// level-0 colour is complete (in `out`).
-__device__ bool finish_node(const KParams& P, Lane& L, Frame* fr, bool hit, v3& out) {
-    v3 child = L.color;
-    if (!hit) child = v3{0.0f, 0.0f, 0.0f};
-    if (hit && L.level < P.max_level) {
-        const DMat m = load_mat(P.S, L.mat);
-        if (m.transp == 1.0f) {
-            if (m.ks[0] > 0.0f || m.ks[1] > 0.0f || m.ks[2] > 0.0f) {
-                Frame& f = fr[L.level];
-                f.color = L.color;
-                f.w = v3{m.ks[0], m.ks[1], m.ks[2]};
-                f.mode = FR_MIRROR;
-                f.flag = (m.shin != 0.0f);
-                if (f.flag && P.glossy_n > 1) {  // lobe samples follow the mirror ray
-                    f.mode = FR_GLOSSY;
-                    f.flag = 0;
-                    f.d2 = L.refl;
-                    f.hp = L.hp;
-                    f.nraw = L.nraw;
-                    f.shin = m.shin;
-                    f.gd = m.gd;
-                }
-                L.qo = L.hp + 0.01f * L.refl;
-                L.qd = L.refl;
-                L.qt = FLT_MAX;
-                L.qtype = Q_PATH;
-                L.level++;
-                return true;
+// A getFinalColor node was hit by the path query (qo, qd): record the shading point, start its
+// light loop and decide its children (src/main.cpp:131-290) -- the mirror or reflected child after
+// the lights (L.desc, weight L.wc), and a frame for a pending refracted ray or a glossy lobe.
+template <bool COUNT, bool TEX>
+__device__ __forceinline__ void begin_node(const KParams& P, Lane& L, Frame* fr, v3 qo, v3 qd, const Best& b,
+                                           Cnt& cnt) {
+    const DevScene& S = P.S;
+    const Surf s = surface(S, qo, qd, b, TEX, L.level == 0);
+    if (COUNT) {
+        cnt.hits++;
+        if (s.ub) cnt.ub++;
+    }
+    L.hp = s.p;
+    L.nN = normalize(s.n);
+    L.refl = reflect(normalize(qd), L.nN);
+    L.nR = normalize(L.refl);
+    L.mat = (b.rec >= 0) ? s.mesh : b.rec;
+    if (TEX) L.kd = v3{s.m.kd[0], s.m.kd[1], s.m.kd[2]};
+    L.color = v3{0.0f, 0.0f, 0.0f};
+    L.lt = L_POINT;
+    L.li = 0;
+    L.ls = -1;
+    L.desc = false;
+    if (L.level >= P.max_level) return;
+    const DMat& m = s.m;
+    const v3 ks{m.ks[0], m.ks[1], m.ks[2]};
+    if (m.transp == 1.0f) {
+        if (!(ks.x > 0.0f || ks.y > 0.0f || ks.z > 0.0f)) return;
+        L.desc = true;
+        if (m.shin != 0.0f) {
+            // color += ks * reflectColor / glossy_ray_count (src/main.cpp:204-251)
+            L.wc = L.w * ((ks * ks) / (float)P.glossy_n);
+            if (P.glossy_n > 1) {
+                Frame& f = fr[L.nfr++];
+                f.mode = FR_GLOSSY;
+                f.o = L.hp;
+                f.d = L.refl;
+                f.w = L.w * (ks / (float)P.glossy_n);
+                f.nraw = s.n;
+                f.shin = m.shin;
+                f.gd = m.gd;
+                f.level = L.level + 1;
+                f.sample = 0;
             }
         } else {
-            const v3 l = normalize(L.cur_d);
-            const v3 n = L.nN;
-            const float r = P.refr;
-            const float c = fabsf(dot(l, n));
-            v3 refr = r * l + (r * c - sqrtf(1.0f - r * r * (1.0f - c * c))) * n;
-            refr = normalize(refr);
-            const float R0 = m.transp;
-            const float reflC = (float)((double)R0 + (double)(1.0f - R0) * pow((double)(1.0f - c), 5.0));
-            const float refrC = 1.0f - reflC;
-            Frame& f = fr[L.level];
-            f.color = L.color;
-            f.w = v3{reflC, refrC, 0.0f};
-            f.o2 = L.hp + 0.01f * refr;
-            f.d2 = refr;
-            f.mode = FR_TRANS_A;
-            f.flag = (r * r * (1.0f - c * c) <= 1.0f);
-            L.qo = L.hp + 0.01f * L.refl;
-            L.qd = L.refl;
-            L.qt = FLT_MAX;
-            L.qtype = Q_PATH;
-            L.level++;
+            L.wc = L.w * (ks * ks);  // color += ks * (0 + ks * child)
+        }
+        return;
+    }
+    // transparent: Schlick Fresnel with R0 = transparency, Snell with eta = refraction_factor
+    // (src/main.cpp:257-290); the reflected child first, then the refracted one (if traced)
+    const v3 l = normalize(qd);
+    const v3 n = L.nN;
+    const float r = P.refr;
+    const float c = fabsf(dot(l, n));
+    v3 refr = r * l + (r * c - sqrtf(1.0f - r * r * (1.0f - c * c))) * n;
+    refr = normalize(refr);
+    const float R0 = m.transp;
+    const float reflC = (float)((double)R0 + (double)(1.0f - R0) * pow((double)(1.0f - c), 5.0));
+    const float refrC = 1.0f - reflC;
+    L.desc = true;
+    L.wc = L.w * reflC;
+    if (r * r * (1.0f - c * c) <= 1.0f) {
+        Frame& f = fr[L.nfr++];
+        f.mode = FR_REFRACT;
+        f.o = L.hp + 0.01f * refr;
+        f.d = refr;
+        f.w = L.w * refrC;
+        f.level = L.level + 1;
+    }
+}
+
+// The subtree under the current node is finished: resume the deepest pending branch (true, query
+// in q) or report the camera sample complete (false, colour in L.acc).
+__device__ __forceinline__ bool next_branch(const KParams& P, Lane& L, Frame* fr, Query& q) {
+    while (L.nfr > 0) {
+        Frame& f = fr[L.nfr - 1];
+        if (f.mode == FR_REFRACT) {
+            L.nfr--;
+            L.level = f.level;
+            L.w = f.w;
+            q.o = f.o;
+            q.d = f.d;
+            q.t = FLT_MAX;
             return true;
         }
-    }
-    while (L.level > 0) {
-        L.level--;
-        Frame& f = fr[L.level];
-        if (f.mode == FR_MIRROR) {
-            const v3 rc = v3{0.0f, 0.0f, 0.0f} + f.w * child;
-            const v3 add = f.flag ? (f.w * rc) / (float)P.glossy_n : f.w * rc;
-            child = f.color + add;
-        } else if (f.mode == FR_GLOSSY) {
-            // reflectColor = 0 + ks * mirror child, then + child * max(pow(dot(reflect, dir), s), 0)
-            // per lobe sample that left the surface (src/main.cpp:197-250)
-            if (f.flag == 0) {
-                f.o2 = v3{0.0f, 0.0f, 0.0f} + f.w * child;
-            } else {
-                const float cw = powf(dot(f.d2, f.sdir), f.shin);
-                f.o2 = f.o2 + child * gmax(cw, 0.0f);
-            }
-            if (glossy_next(P, L, f)) {
-                L.level++;
-                return true;
-            }
-            child = f.color + (f.w * f.o2) / (float)P.glossy_n;
-        } else if (f.mode == FR_TRANS_A) {
-            f.color = f.color + f.w.x * child;
-            if (f.flag) {
-                f.mode = FR_TRANS_B;
-                L.qo = f.o2;
-                L.qd = f.d2;
-                L.qt = FLT_MAX;
-                L.qtype = Q_PATH;
-                L.level++;
-                return true;
-            }
-            child = f.color;
-        } else {
-            child = f.color + f.w.y * child;
+        float cw;
+        if (glossy_next(P, L, f, q, cw)) {  // reflectColor += child * cw (src/main.cpp:239-240)
+            L.level = f.level;
+            L.w = f.w * cw;
+            return true;
         }
+        L.nfr--;
     }
-    out = child;
     return false;
 }
 
@@ -715,9 +585,9 @@ struct JobSrc {
     int mode;  // 0: pixels of the band layout, 1: explicit rays (rt_shade)
     int njobs;
     const rt_ray* rays;
-    float* rgb;                    // mode 1 output [n][3]
+    float* rgb;                      // mode 1 output [n][3]
     unsigned long long* ray_counts;  // mode 1 per-ray counts
-    int* counter;                  // global job counter (zeroed per launch)
+    int* counter;                    // global job counter (zeroed per launch)
     int* xq;  // dynamic-fetch kernel, or null: 8 job heads (32-int spacing, zeroed per launch), one
               // per group of blocks sharing an XCD (blockIdx % 8), each over 1/8 of the jobs
     int n_views;    // view batch: njobs = n_views * view_jobs
@@ -746,10 +616,22 @@ __device__ __forceinline__ int view_job(const KParams& P, int g, int& v) {
     return lo + (k - v * (hi - lo));
 }
 
+// a new camera sample or explicit ray: the root of a fresh recursion tree
+__device__ __forceinline__ void new_tree(Lane& L) {
+    L.acc = v3{0.0f, 0.0f, 0.0f};
+    L.w = v3{1.0f, 1.0f, 1.0f};
+    L.level = 0;
+    L.nfr = 0;
+    L.draws = 0u;
+    L.shadow = false;
+}
+
 // queue the camera ray of the lane's current sample (src/main.cpp:350-386)
-__device__ __forceinline__ void queue_camera(const KParams& P, Lane& L) {
-    const float ndx = (float)L.px / (float)P.W * 2.0f - 1.0f;
-    const float ndy = (float)L.py / (float)P.H * 2.0f - 1.0f;
+__device__ __forceinline__ void queue_camera(const KParams& P, Lane& L, Query& q) {
+    const int py = (int)(L.rpix / (uint32_t)P.W);
+    const int px = (int)(L.rpix - (uint32_t)py * (uint32_t)P.W);
+    const float ndx = (float)px / (float)P.W * 2.0f - 1.0f;
+    const float ndy = (float)py / (float)P.H * 2.0f - 1.0f;
     float sx = ndx, sy = ndy;
     if (P.aa) {
         const int s = L.sample;
@@ -757,28 +639,22 @@ __device__ __forceinline__ void queue_camera(const KParams& P, Lane& L) {
         sy = (s < 2) ? ndy + P.aa_offy : ndy - P.aa_offy;
     } else if (P.multi) {
         const int per_q = ((P.ms_moves + 1) / 2) * ((P.ms_moves + 1) / 2);
-        const int q = L.sample / per_q;
+        const int qd = L.sample / per_q;
         const int r = L.sample % per_q;
         const int nyv = (P.ms_moves + 1) / 2;
         const int xx = 1 + 2 * (r / nyv);
         const int yy = 1 + 2 * (r % nyv);
-        const float qx = (q == 0 || q == 2) ? -1.0f : 1.0f;
-        const float qy = (q < 2) ? 1.0f : -1.0f;
+        const float qx = (qd == 0 || qd == 2) ? -1.0f : 1.0f;
+        const float qy = (qd < 2) ? 1.0f : -1.0f;
         sx = ndx + (P.ms_offx * qx * (float)xx);
         sy = ndy + (P.ms_offy * qy * (float)yy);
     }
-    v3 o, d;
     if (P.n_views > 1)
-        gen_ray_view(P, L.out_row / P.view_rows, sx, sy, o, d);
+        gen_ray_view(P, L.out_row / P.view_rows, sx, sy, q.o, q.d);
     else
-        gen_ray(P, sx, sy, o, d);
-    L.qo = o;
-    L.qd = d;
-    L.qt = FLT_MAX;
-    L.qtype = Q_PATH;
-    L.level = 0;
-    L.draws = 0u;
-    L.rpix = (uint32_t)(L.py * P.W + L.px);  // the reference's pixel (x, y), y up
+        gen_ray(P, sx, sy, q.o, q.d);
+    q.t = FLT_MAX;
+    new_tree(L);
 }
 
 // Map a job index to its pixel (8x8 tiles inside the rank's bands).  False if outside the image.
@@ -795,14 +671,153 @@ __device__ __forceinline__ bool job_pixel(const KParams& P, int gjob, Lane& L) {
     const int lb = rest / tiles_y_band;
     const int gb = lb * P.band_count + P.band_rank;
     const int row_in_band = ty * 8 + (lane >> 3);
-    L.px = tx * 8 + (lane & 7);
-    L.py = gb * P.band_rows + row_in_band;
+    const int px = tx * 8 + (lane & 7);
+    const int py = gb * P.band_rows + row_in_band;
+    L.rpix = (uint32_t)(py * P.W + px);  // the reference's pixel (x, y), y up
     L.out_row = view * P.view_rows + lb * P.band_rows + row_in_band;
-    return (L.px < P.W) && (row_in_band < P.band_rows) && (L.py < P.H) && (lb < P.n_local_bands);
+    return (px < P.W) && (row_in_band < P.band_rows) && (py < P.H) && (lb < P.n_local_bands);
 }
 
-template <bool COUNT, int WPE, int BW, bool TEX = true>
-__global__ __launch_bounds__(64, WPE) void persistent_kernel(KParams P, JobSrc J) {
+// Start job `job` on the lane: its first query in q.  False for a padding pixel (the lane stays
+// idle and fetches again).
+__device__ __forceinline__ bool start_job(const KParams& P, const JobSrc& J, Lane& L, int job, Query& q) {
+    L.job = job;
+    L.sample = 0;
+    L.pacc = v3{0.0f, 0.0f, 0.0f};
+    if (J.mode == 0) {
+        if (!job_pixel(P, job, L)) {
+            L.job = -1;
+            return false;
+        }
+        queue_camera(P, L, q);
+        return true;
+    }
+    const rt_ray r = J.rays[job];
+    q.o = v3{r.origin[0], r.origin[1], r.origin[2]};
+    q.d = v3{r.direction[0], r.direction[1], r.direction[2]};
+    q.t = r.t;
+    L.rpix = (uint32_t)job;
+    new_tree(L);
+    return true;
+}
+
+// The state-machine advance after a finished query (q = that query's ray; hit, b = its result):
+// the cansee segment loop, the light loop, the recursion tree, the camera samples and the pixel
+// output.  Returns true with the next query in q (L.shadow says which kind); false when the lane's
+// job is complete (L.job = -1).
+template <bool COUNT, bool TEX>
+__device__ __forceinline__ bool advance_lane(const KParams& P, const JobSrc& J, Lane& L, Frame* fr, bool hit, const Best& b,
+                             Query& q, Cnt& cnt, uint32_t job_rays) {
+    const DevScene& S = P.S;
+    bool lights_have = false, lights_vis = false;
+    if (L.shadow) {
+        // one cansee segment (src/shadow.cpp:41-67)
+        bool vis;
+        if (S.all_opaque) {
+            vis = !hit;
+        } else if (!hit || b.t > L.sdist - 2.0f * 0.0005f) {
+            vis = true;
+        } else {
+            const Surf s = surface(S, q.o, q.d, b);
+            if (s.m.transp != 1.0f) {
+                L.sdist -= b.t;
+                const float c = fabsf(dot(q.d, s.n));
+                const float R0 = s.m.transp;
+                L.sI = (float)((double)L.sI *
+                               (1.0 - ((double)R0 + (double)(1.0f - R0) * pow((double)(1.0f - c), 5.0))));
+                if (L.sdist > 0.0005f) {
+                    q.o = s.p + 0.0005f * q.d;  // the next segment, same direction
+                    q.t = FLT_MAX;
+                    return true;
+                }
+                vis = true;  // loop exit without an opaque blocker
+            } else {
+                vis = false;
+            }
+        }
+        lights_have = true;
+        lights_vis = vis;
+    } else if (hit) {
+        begin_node<COUNT, TEX>(P, L, fr, q.o, q.d, b, cnt);
+    }
+    bool more;
+    if (L.shadow || hit) {
+        L.shadow = false;
+        if (advance_lights<TEX>(P, L, lights_have, lights_vis, q)) return true;
+        // every light done: the node's colour, then its mirror / reflected child
+        L.acc = L.acc + L.w * L.color;
+        if (L.desc) {
+            L.w = L.wc;
+            L.level++;
+            q.o = L.hp + 0.01f * L.refl;
+            q.d = L.refl;
+            q.t = FLT_MAX;
+            return true;
+        }
+        more = next_branch(P, L, fr, q);
+    } else {
+        more = next_branch(P, L, fr, q);  // a miss: getFinalColor returns black
+    }
+    if (more) return true;
+    // camera sample complete
+    if (J.mode == 0) {
+        if (P.aa || P.multi) L.pacc += L.acc;
+        else L.pacc = L.acc;
+        L.sample++;
+        const int nsamples = P.aa ? 4 : (P.multi ? P.sample_size : 1);
+        if (L.sample < nsamples) {
+            queue_camera(P, L, q);
+            return true;
+        }
+        v3 col = L.pacc;
+        if (P.aa) col = L.pacc * 0.25f;
+        else if (P.multi) col = L.pacc * (float)(1.0f / (float)P.sample_size);
+        const int py = (int)(L.rpix / (uint32_t)P.W);
+        const int px = (int)(L.rpix - (uint32_t)py * (uint32_t)P.W);
+        float* dst = P.out + ((size_t)L.out_row * P.W + px) * 3;
+        dst[0] = col.x;
+        dst[1] = col.y;
+        dst[2] = col.z;
+    } else {
+        J.rgb[L.job * 3 + 0] = L.acc.x;
+        J.rgb[L.job * 3 + 1] = L.acc.y;
+        J.rgb[L.job * 3 + 2] = L.acc.z;
+        J.ray_counts[L.job] = job_rays;
+    }
+    L.job = -1;
+    return false;
+}
+
+// The same advance as an out-of-line call: the lane's state then lives in the call's private frame
+// between queries instead of in registers across the traversal loop (kernel variant bit RT_V_CALL).
+template <bool COUNT, bool TEX>
+__device__ __attribute__((noinline)) bool advance_lane_call(const KParams& P, const JobSrc& J, Lane& L, Frame* fr,
+                                                            bool hit, const Best& b, Query& q, Cnt& cnt,
+                                                            uint32_t job_rays) {
+    return advance_lane<COUNT, TEX>(P, J, L, fr, hit, b, q, cnt, job_rays);
+}
+
+// Kernel variants (compile-time): bit 0 RT_V_CALL = state machine out of line; bit 1 RT_V_NOPF = no
+// node prefetch in the dynamic-fetch traversal; bit 2 RT_V_NOCOOP = no drain lane groups; bit 3
+// RT_V_W3 = compiled for 3 waves per SIMD (168 VGPRs) instead of 2 (256).  Every variant renders the
+// same bits; they differ in registers, spills and occupancy.
+#define RT_V_CALL 1
+#define RT_V_NOPF 2
+#define RT_V_NOCOOP 4
+#define RT_V_W3 8
+
+template <bool COUNT, bool TEX, int V>
+__device__ __forceinline__ bool advance_v(const KParams& P, const JobSrc& J, Lane& L, Frame* fr, bool hit, const Best& b,
+                                          Query& q, Cnt& cnt, uint32_t job_rays) {
+    if (V & RT_V_CALL) return advance_lane_call<COUNT, TEX>(P, J, L, fr, hit, b, q, cnt, job_rays);
+    return advance_lane<COUNT, TEX>(P, J, L, fr, hit, b, q, cnt, job_rays);
+}
+
+// ---- whole-traversal persistent kernel ------------------------------------------------------
+// Refill between whole traversals: every busy lane traces its query with trace_query8, then
+// advances; idle lanes take jobs (one atomic per wave).
+template <bool COUNT, bool TEX, int V>
+__global__ __launch_bounds__(64, (V & RT_V_W3) ? 3 : 2) void persistent_kernel(KParams P, JobSrc J) {
     __shared__ int stack_lds[RT_STACK_SIZE * RT_WAVE];
     __shared__ int s_base;
     const int lane_id = threadIdx.x;
@@ -813,14 +828,15 @@ __global__ __launch_bounds__(64, WPE) void persistent_kernel(KParams P, JobSrc J
     Frame fr[RT_MAX_DEPTH];
     Lane L;
     L.job = -1;
-    Cnt cnt{0u, 0u, 0u, 0u};
-    Cnt job_cnt{0u, 0u, 0u, 0u};  // per-job ray count (rt_shade)
+    L.shadow = false;
+    L.sdist = 0.0f;
+    Query q;
+    Cnt cnt{};
+    uint32_t job_rays = 0;  // queries of the lane's current job (rt_shade ray counts)
     bool need_trace = false;
-    bool pre = false;  // the queued camera query's hit is precomputed (primary packet pass)
-    Best pb;
     for (;;) {
         // ---- refill idle lanes (one atomic per wave) ----
-        const bool idle = (L.job < 0);
+        const bool idle = (L.job == -1);
         const unsigned long long want = __ballot(idle);
         if (want) {
             if (lane_id == __ffsll((long long)want) - 1) s_base = atomicAdd(J.counter, __popcll(want));
@@ -829,43 +845,10 @@ __global__ __launch_bounds__(64, WPE) void persistent_kernel(KParams P, JobSrc J
             __syncthreads();
             const int base = s_base;
             if (idle) {
-                const int myrank = __popcll(want & ((1ull << lane_id) - 1ull));
-                const int job_k = base + myrank;
+                const int job_k = base + __popcll(want & ((1ull << lane_id) - 1ull));
                 if (job_k < J.njobs) {
-                    const int job = P.job_order ? P.job_order[job_k] : job_k;  // longest-first order
-                    L.job = job;
-                    L.sample = 0;
-                    L.pacc = v3{0.0f, 0.0f, 0.0f};
-                    job_cnt.rays = 0u;
-                    if (J.mode == 0) {
-                        if (!job_pixel(P, job, L)) {
-                            L.job = -1;  // padding pixel: nothing to do, fetch again next round
-                        } else {
-                            L.nsamples = P.aa ? 4 : (P.multi ? P.sample_size : 1);
-                            queue_camera(P, L);
-                            need_trace = true;
-                            if (P.pre_rec) {
-                                const int r = P.pre_rec[job];
-                                if (r != RT_PRE_NONE) {
-                                    pre = true;
-                                    pb.t = P.pre_t[job];
-                                    pb.rec = r;
-                                    pb.key = 0;
-                                }
-                            }
-                        }
-                    } else {
-                        const rt_ray r = J.rays[job];
-                        L.nsamples = 1;
-                        L.qo = v3{r.origin[0], r.origin[1], r.origin[2]};
-                        L.qd = v3{r.direction[0], r.direction[1], r.direction[2]};
-                        L.qt = r.t;
-                        L.qtype = Q_PATH;
-                        L.level = 0;
-                        L.draws = 0u;
-                        L.rpix = (uint32_t)job;
-                        need_trace = true;
-                    }
+                    need_trace = start_job(P, J, L, job_k, q);
+                    job_rays = 0;
                 } else {
                     L.job = -2;  // no more work for this lane
                 }
@@ -880,125 +863,19 @@ __global__ __launch_bounds__(64, WPE) void persistent_kernel(KParams P, JobSrc J
         // ---- the one traversal ----
         Best b;
         bool hit = false;
-        if (busy && pre) {
-            b = pb;
-            hit = (pb.rec != RT_NO_HIT);
-            pre = false;
-        } else if (busy) {
+        if (busy) {
             cnt.rays++;
-            job_cnt.rays++;
-            const bool shadow = (L.qtype == Q_SHADOW);
-            const bool ref = shadow || P.use_bvh;
-            const bool any = shadow && S.all_opaque;
-            const float thr = L.sdist - 2.0f * 0.0005f;
-            if (BW > 2)
-                hit = trace_query8<COUNT, BW>(S, L.qo, L.qd, L.qt, thr, ref, any, b, stk, cnt);
-            else
-                hit = trace_query<COUNT>(S, L.qo, L.qd, L.qt, thr, ref, any, b, stk, cnt);
+            job_rays++;
+            hit = trace_query8<COUNT, 8>(S, q.o, q.d, q.t, L.sdist - 2.0f * 0.0005f, L.shadow || P.use_bvh,
+                                         L.shadow && S.all_opaque, b, stk, cnt);
         }
         if (!busy) continue;
         if (COUNT && wave_leader()) cnt.wadv++;
         // ---- advance the state machine until the next query ----
-        // Each step below has exactly one call site (advance_lights, finish_node, pixel output):
-        // inlined twice, the light loop and the recursion fold pushed the kernel past 256 VGPRs.
-        need_trace = false;
-        bool run_lights = false, lights_have = false, lights_vis = false;
-        bool node_hit = true;
-        if (L.qtype == Q_SHADOW) {
-            bool vis;
-            bool again = false;
-            if (S.all_opaque) {
-                vis = !hit;
-            } else if (!hit || b.t > L.sdist - 2.0f * 0.0005f) {
-                vis = true;
-            } else {
-                const Surf s = surface(S, L.qo, L.qd, b);
-                if (s.m.transp != 1.0f) {
-                    L.sdist -= b.t;
-                    L.so = s.p + 0.0005f * L.sd;
-                    const float c = fabsf(dot(L.sd, s.n));
-                    const float R0 = s.m.transp;
-                    L.sI = (float)((double)L.sI *
-                                   (1.0 - ((double)R0 + (double)(1.0f - R0) * pow((double)(1.0f - c), 5.0))));
-                    if (L.sdist > 0.0005f) {
-                        L.qo = L.so;
-                        L.qd = L.sd;
-                        L.qt = FLT_MAX;
-                        again = true;
-                    }
-                    vis = true;  // loop exit without an opaque blocker
-                } else {
-                    vis = false;
-                }
-            }
-            if (again) {
-                need_trace = true;
-                continue;
-            }
-            run_lights = true;
-            lights_have = true;
-            lights_vis = vis;
-        } else {
-            // a getFinalColor node (src/main.cpp:131-190)
-            L.cur_d = L.qd;
-            if (!hit) {
-                L.color = v3{0.0f, 0.0f, 0.0f};
-                node_hit = false;
-            } else {
-                if (COUNT) cnt.hits++;
-                const Surf s = surface(S, L.qo, L.qd, b, TEX, L.level == 0);
-                L.hp = s.p;
-                L.nraw = s.n;
-                L.nN = normalize(s.n);
-                L.refl = reflect(normalize(L.qd), L.nN);
-                L.nR = normalize(L.refl);
-                L.mat = (b.rec >= 0) ? s.mesh : b.rec;
-            if (TEX) fr[L.level].kd = v3{s.m.kd[0], s.m.kd[1], s.m.kd[2]};
-                L.color = v3{0.0f, 0.0f, 0.0f};
-                L.lt = L_POINT;
-                L.li = 0;
-                L.ls = -1;
-                run_lights = true;
-            }
-        }
-        if (run_lights && advance_lights<TEX>(P, L, fr, lights_have, lights_vis)) {
-            need_trace = true;
-            continue;
-        }
-        // every light done (or a miss): fold the node into the recursion tree
-        v3 out;
-        if (finish_node(P, L, fr, node_hit, out)) {
-            need_trace = true;
-            continue;
-        }
-        // level-0 colour complete
-        if (J.mode == 0) {
-            if (P.aa || P.multi) L.pacc += out;
-            else L.pacc = out;
-            L.sample++;
-            if (L.sample < L.nsamples) {
-                queue_camera(P, L);
-                need_trace = true;
-                continue;
-            }
-            v3 col = L.pacc;
-            if (P.aa) col = L.pacc * 0.25f;
-            else if (P.multi) col = L.pacc * (float)(1.0f / (float)P.sample_size);
-            float* dst = P.out + ((size_t)L.out_row * P.W + L.px) * 3;
-            dst[0] = col.x;
-            dst[1] = col.y;
-            dst[2] = col.z;
-            if (P.job_cost) P.job_cost[L.job] = (int)job_cnt.rays;  // queries of this pixel (schedule)
-        } else {
-            J.rgb[L.job * 3 + 0] = out.x;
-            J.rgb[L.job * 3 + 1] = out.y;
-            J.rgb[L.job * 3 + 2] = out.z;
-            J.ray_counts[L.job] = job_cnt.rays;
-        }
-        L.job = -1;
+        need_trace = advance_v<COUNT, TEX, V>(P, J, L, fr, hit, b, q, cnt, job_rays);
     }
     flush_counters<COUNT>(P, cnt);
-    if (P.wave_trace && lane_id == 0) {  // RT_WAVE_TRACE: (start, end, jobs) per wave, 100 MHz clock
+    if (P.wave_trace && lane_id == 0) {  // wave trace: (start, end, jobs) per wave, 100 MHz clock
         unsigned long long* w = P.wave_trace + 8 * blockIdx.x;
         w[0] = t_wave0;
         w[1] = wall_clock64();
@@ -1007,8 +884,7 @@ __global__ __launch_bounds__(64, WPE) void persistent_kernel(KParams P, JobSrc J
     }
 }
 
-
-// ---- dynamic-fetch persistent kernel (quantised BVH8/BVH4) ------------------------------------
+// ---- dynamic-fetch persistent kernel --------------------------------------------------------
 // persistent_kernel above refills a lane only between whole traversals, so a wave runs every
 // traversal for as long as its slowest query: on the dragon ~1/5 of the lanes are active per
 // node fetch.  Here the traversal is a resumable per-lane state (Trav) advanced one node visit
@@ -1035,7 +911,7 @@ struct Trav {
 
 __device__ __forceinline__ bool leaf_pending(const Trav& T) { return T.rk > 0 || T.lh != 0u; }
 
-// Query setup: the prologue of trace_query8 / trace_query (same thresholds and flags).
+// Query setup: the prologue of trace_query8 (same thresholds and flags).
 __device__ __forceinline__ void trav_init_q(const DevScene& S, bool use_bvh, v3 qo, v3 qd, float qt, bool shadow,
                                             float sdist, Trav& T) {
     T.o = qo;
@@ -1067,9 +943,6 @@ __device__ __forceinline__ void trav_init_q(const DevScene& S, bool use_bvh, v3 
     }
 }
 
-__device__ __forceinline__ void trav_init(const KParams& P, const Lane& L, Trav& T) {
-    trav_init_q(P.S, P.use_bvh != 0, L.qo, L.qd, L.qt, L.qtype == Q_SHADOW, L.sdist, T);
-}
 
 __device__ __forceinline__ void node_fetch(const float4* nodes, uint32_t cur, float4 (&g)[8]) {
     const float4* np = nodes + (size_t)(cur >> 8) * 8;
@@ -1230,10 +1103,22 @@ __device__ __forceinline__ void coop_put(const Trav& T, int* q, int r) {
 
 // the owner's query after coop_group_trace: its hit, nothing left to walk
 __device__ __forceinline__ void coop_get(Trav& T, const int* q, int r) {
+    // every field the finished query still needs comes back from LDS, so the owner's traversal
+    // registers are dead across coop_group_trace
+    T.o = v3{__int_as_float(q[CQ_OX * COOP_Q + r]), __int_as_float(q[CQ_OY * COOP_Q + r]),
+             __int_as_float(q[CQ_OZ * COOP_Q + r])};
+    T.d = v3{__int_as_float(q[CQ_DX * COOP_Q + r]), __int_as_float(q[CQ_DY * COOP_Q + r]),
+             __int_as_float(q[CQ_DZ * COOP_Q + r])};
+    T.nd = v3{__int_as_float(q[CQ_NX * COOP_Q + r]), __int_as_float(q[CQ_NY * COOP_Q + r]),
+              __int_as_float(q[CQ_NZ * COOP_Q + r])};
+    T.thr = __int_as_float(q[CQ_THR * COOP_Q + r]);
     T.best.t = __int_as_float(q[CQ_BT * COOP_Q + r]);
     T.best.key = q[CQ_BKEY * COOP_Q + r];
     T.best.rec = q[CQ_BREC * COOP_Q + r];
-    T.found = (q[CQ_FLAGS * COOP_Q + r] & 1) != 0;
+    const int flags = q[CQ_FLAGS * COOP_Q + r];
+    T.found = (flags & 1) != 0;
+    T.ref = (flags & 2) != 0;
+    T.any = (flags & 4) != 0;
     T.tcull = __int_as_float(q[CQ_TCULL * COOP_Q + r]);
     T.mask.known = (uint32_t)q[CQ_MK * COOP_Q + r];
     T.mask.pass = (uint32_t)q[CQ_MP * COOP_Q + r];
@@ -1481,99 +1366,9 @@ __device__ __forceinline__ void trav_finish(const DevScene& S, Trav& T) {
     }
 }
 
-// The state-machine advance of persistent_kernel after a finished query (shadow segment,
-// light loop, recursion fold, pixel output).  Returns true with the next query in L.q*; false
-// when the lane's job is complete (L.job = -1).
-template <bool COUNT, bool TEX = true>
-__device__ bool advance_lane(const KParams& P, const JobSrc& J, Lane& L, Frame* fr, bool hit, const Best& b,
-                             Cnt& cnt, const Cnt& job_cnt) {
-    const DevScene& S = P.S;
-    bool run_lights = false, lights_have = false, lights_vis = false;
-    bool node_hit = true;
-    if (L.qtype == Q_SHADOW) {
-        bool vis;
-        if (S.all_opaque) {
-            vis = !hit;
-        } else if (!hit || b.t > L.sdist - 2.0f * 0.0005f) {
-            vis = true;
-        } else {
-            const Surf s = surface(S, L.qo, L.qd, b);
-            if (s.m.transp != 1.0f) {
-                L.sdist -= b.t;
-                L.so = s.p + 0.0005f * L.sd;
-                const float c = fabsf(dot(L.sd, s.n));
-                const float R0 = s.m.transp;
-                L.sI = (float)((double)L.sI *
-                               (1.0 - ((double)R0 + (double)(1.0f - R0) * pow((double)(1.0f - c), 5.0))));
-                if (L.sdist > 0.0005f) {
-                    L.qo = L.so;
-                    L.qd = L.sd;
-                    L.qt = FLT_MAX;
-                    return true;
-                }
-                vis = true;  // loop exit without an opaque blocker
-            } else {
-                vis = false;
-            }
-        }
-        run_lights = true;
-        lights_have = true;
-        lights_vis = vis;
-    } else {
-        // a getFinalColor node (src/main.cpp:131-190)
-        L.cur_d = L.qd;
-        if (!hit) {
-            L.color = v3{0.0f, 0.0f, 0.0f};
-            node_hit = false;
-        } else {
-            if (COUNT) cnt.hits++;
-            const Surf s = surface(S, L.qo, L.qd, b, TEX, L.level == 0);
-            L.hp = s.p;
-            L.nraw = s.n;
-            L.nN = normalize(s.n);
-            L.refl = reflect(normalize(L.qd), L.nN);
-            L.nR = normalize(L.refl);
-            L.mat = (b.rec >= 0) ? s.mesh : b.rec;
-            if (TEX) fr[L.level].kd = v3{s.m.kd[0], s.m.kd[1], s.m.kd[2]};
-            L.color = v3{0.0f, 0.0f, 0.0f};
-            L.lt = L_POINT;
-            L.li = 0;
-            L.ls = -1;
-            run_lights = true;
-        }
-    }
-    if (run_lights && advance_lights<TEX>(P, L, fr, lights_have, lights_vis)) return true;
-    v3 out;
-    if (finish_node(P, L, fr, node_hit, out)) return true;
-    // level-0 colour complete
-    if (J.mode == 0) {
-        if (P.aa || P.multi) L.pacc += out;
-        else L.pacc = out;
-        L.sample++;
-        if (L.sample < L.nsamples) {
-            queue_camera(P, L);
-            return true;
-        }
-        v3 col = L.pacc;
-        if (P.aa) col = L.pacc * 0.25f;
-        else if (P.multi) col = L.pacc * (float)(1.0f / (float)P.sample_size);
-        float* dst = P.out + ((size_t)L.out_row * P.W + L.px) * 3;
-        dst[0] = col.x;
-        dst[1] = col.y;
-        dst[2] = col.z;
-        if (P.job_cost) P.job_cost[L.job] = (int)job_cnt.rays;  // queries of this pixel (schedule)
-    } else {
-        J.rgb[L.job * 3 + 0] = out.x;
-        J.rgb[L.job * 3 + 1] = out.y;
-        J.rgb[L.job * 3 + 2] = out.z;
-        J.ray_counts[L.job] = job_cnt.rays;
-    }
-    L.job = -1;
-    return false;
-}
-
-template <bool COUNT, int WPE, int BW, bool TEX = true>
-__global__ __launch_bounds__(64, WPE) void persistent_df_kernel(KParams P, JobSrc J) {
+template <bool COUNT, bool TEX, int V>
+__global__ __launch_bounds__(64, (V & RT_V_W3) ? 3 : 2) void persistent_df_kernel(KParams P, JobSrc J) {
+    constexpr bool PF = !(V & RT_V_NOPF), COOP = !(V & RT_V_NOCOOP);
     __shared__ int stack_lds[RT_STACK8 * RT_WAVE];
     __shared__ int coop_pool[COOP_POOL];   // drain: node groups of the wave's last queries
     __shared__ int coop_q[CQ_N * COOP_Q];  // drain: those queries
@@ -1586,14 +1381,15 @@ __global__ __launch_bounds__(64, WPE) void persistent_df_kernel(KParams P, JobSr
     Frame fr[RT_MAX_DEPTH];
     Lane L;
     L.job = -1;
+    L.shadow = false;
+    L.sdist = 0.0f;
     Trav T;
-    Cnt cnt{0u, 0u, 0u, 0u};
-    Cnt job_cnt{0u, 0u, 0u, 0u};  // per-job ray count (rt_shade)
+    Cnt cnt{};
+    uint32_t job_rays = 0;                       // queries of the lane's current job (rt_shade ray counts)
     int xr = (int)(blockIdx.x & 7), xtried = 0;  // J.xq: the job range this wave draws from, ranges used up
-    bool tracing = false;          // a query is in flight
-    bool pending = false;          // a finished query waits for advance_lane
+    bool tracing = false;                        // a query is in flight
+    bool pending = false;                        // a finished query waits for advance_lane
     const int refill_at = P.refill;
-    const int leaf_batch = P.leaf_batch;
     // wave trace of the drain (after this wave first found the job queue empty)
     unsigned long long t_exh = 0ull;
     unsigned int it_drain = 0, lanes_drain = 0, coop_n = 0, pa_drain = 0;
@@ -1602,10 +1398,13 @@ __global__ __launch_bounds__(64, WPE) void persistent_df_kernel(KParams P, JobSr
         unsigned long long tA = COUNT ? (unsigned long long)clock64() : 0ull;
         if (P.wave_trace && t_exh) pa_drain++;
         bool start = false;
+        Query q;
         if (pending) {
             pending = false;
             if (COUNT && wave_leader()) cnt.wadv++;
-            start = advance_lane<COUNT, TEX>(P, J, L, fr, T.found, T.best, cnt, job_cnt);
+            q.o = T.o;
+            q.d = T.d;
+            start = advance_v<COUNT, TEX, V>(P, J, L, fr, T.found, T.best, q, cnt, job_rays);
         }
         const unsigned long long tJ = COUNT ? (unsigned long long)clock64() : 0ull;
         if (COUNT) cnt.cyc_c += tJ - tA;  // state machine
@@ -1634,42 +1433,8 @@ __global__ __launch_bounds__(64, WPE) void persistent_df_kernel(KParams P, JobSr
             if (idle) {
                 const int job_k = base + __popcll(want & ((1ull << lane_id) - 1ull));
                 if (job_k < lim) {
-                    const int job = P.job_order ? P.job_order[job_k] : job_k;  // longest-first order
-                    L.job = job;
-                    L.sample = 0;
-                    L.pacc = v3{0.0f, 0.0f, 0.0f};
-                    job_cnt.rays = 0u;
-                    if (J.mode == 0) {
-                        if (!job_pixel(P, job, L)) {
-                            L.job = -1;  // padding pixel: nothing to do, fetch again next round
-                        } else {
-                            L.nsamples = P.aa ? 4 : (P.multi ? P.sample_size : 1);
-                            queue_camera(P, L);
-                            start = true;
-                            if (P.pre_rec) {
-                                const int r = P.pre_rec[job];
-                                if (r != RT_PRE_NONE) {  // primary hit known: straight to phase A
-                                    start = false;
-                                    T.found = (r != RT_NO_HIT);
-                                    T.best.t = P.pre_t[job];
-                                    T.best.rec = r;
-                                    T.best.key = 0;
-                                    pending = true;
-                                }
-                            }
-                        }
-                    } else {
-                        const rt_ray r = J.rays[job];
-                        L.nsamples = 1;
-                        L.qo = v3{r.origin[0], r.origin[1], r.origin[2]};
-                        L.qd = v3{r.direction[0], r.direction[1], r.direction[2]};
-                        L.qt = r.t;
-                        L.qtype = Q_PATH;
-                        L.level = 0;
-                        L.draws = 0u;
-                        L.rpix = (uint32_t)job;
-                        start = true;
-                    }
+                    start = start_job(P, J, L, job_k, q);
+                    job_rays = 0;
                 } else {
                     L.job = (J.xq && xtried < 8) ? -1 : -2;  // -2: no more work for this lane
                 }
@@ -1679,8 +1444,8 @@ __global__ __launch_bounds__(64, WPE) void persistent_df_kernel(KParams P, JobSr
         if (COUNT) cnt.cyc_d += (unsigned long long)clock64() - tJ;  // job fetch and camera rays
         if (start) {
             cnt.rays++;
-            job_cnt.rays++;
-            trav_init(P, L, T);
+            job_rays++;
+            trav_init_q(S, P.use_bvh != 0, q.o, q.d, q.t, L.shadow, L.sdist, T);
             tracing = true;
         }
         if (P.wave_trace && !t_exh && __any(L.job == -2)) t_exh = wall_clock64();
@@ -1688,79 +1453,21 @@ __global__ __launch_bounds__(64, WPE) void persistent_df_kernel(KParams P, JobSr
             if (!__any(L.job == -1 || pending)) break;  // every lane exhausted
             continue;
         }
-        // ---- phase B: node visits with postponed leaves (while-while), until enough lanes
-        // wait for phase A ----
+        // ---- phase B: one node visit or one leaf record per lane and iteration ("if-if"), until
+        // enough lanes wait for phase A ----
         unsigned long long tB = 0ull;
         if (COUNT) {
             tB = (unsigned long long)clock64();
             cnt.cyc_a += tB - tA;
         }
         float4 g[8];
-        if (tracing && T.cur != RT_TRAV_NONE) node_fetch(S.nodes, T.cur, g);
+        if (PF && tracing && T.cur != RT_TRAV_NONE) node_fetch(S.nodes, T.cur, g);
         for (;;) {
-            if (leaf_batch == 0) {
-                // if-if: every tracing lane takes one step per iteration, a leaf record if it
-                // has postponed ones, else a node visit
-                if (tracing) {
-                    if (leaf_pending(T))
-                        trav_record<COUNT>(S, T, cnt);
-                    else if (T.cur != RT_TRAV_NONE)
-                        trav_node<COUNT, BW>(S, T, stk, g, cnt);
-                }
-                if (tracing && !leaf_pending(T) && T.cur == RT_TRAV_NONE) {
-                    trav_finish(S, T);
-                    tracing = false;
-                    pending = true;
-                }
-                if (!__any(tracing)) break;
-                if (__popcll(__ballot(pending || L.job == -1)) >= refill_at) break;
-                if (P.wave_trace && t_exh) {
-                    it_drain++;
-                    lanes_drain += (unsigned int)__popcll(__ballot(tracing));
-                }
-                // drain (no lane can take a new job): the remaining queries go to lane groups
-                // (coop 2: also in steady state, for the last queries a full-wave refill waits for)
-                if (P.coop && ((P.coop == 2 && refill_at == 64) || (!__any(L.job == -1) && __any(L.job == -2)))) {
-                    const unsigned long long om = __ballot(tracing);
-                    const int k = __popcll(om);
-                    if (k <= P.coop_max) {
-                        int G = 64;
-                        while (G > 1 && k * G > 64) G >>= 1;
-                        const int r = __popcll(om & ((1ull << lane_id) - 1ull));
-                        if (tracing) {
-                            coop_put(T, coop_q, r);
-                            int* gp = coop_pool + r * (COOP_POOL * G / 64);
-                            for (int j = 0; j < T.sp; ++j) gp[j] = stk[j * RT_WAVE];
-                            if (T.cur != RT_TRAV_NONE) gp[T.sp] = (int)T.cur;
-                        }
-                        __syncthreads();
-                        const uint2 nv = coop_group_trace<BW>(S.nodes, S.tri, S.refn, S.leaf_path, coop_pool, coop_q,
-                                                              om, P.coop_reserve);
-                        __syncthreads();
-                        if (COUNT) {
-                            cnt.nodes += nv.x;
-                            cnt.tris += nv.y;
-                        }
-                        if (tracing) coop_get(T, coop_q, r);
-                        if (P.wave_trace) coop_n++;
-                    }
-                }
-                continue;
-            }
-            const bool visit = tracing && !leaf_pending(T) && T.cur != RT_TRAV_NONE;
-            if (visit) trav_node<COUNT, BW>(S, T, stk, g, cnt);
-            // the leaf phase runs once no lane can visit a node without first testing its
-            // postponed leaves, or once `leaf_batch` lanes have some
-            const bool lp = tracing && leaf_pending(T);
-            const bool more_nodes = __any(tracing && !leaf_pending(T) && T.cur != RT_TRAV_NONE);
-            if (__any(lp) && (!more_nodes || __popcll(__ballot(lp)) >= leaf_batch)) {
-                bool work = lp;
-                while (__any(work)) {
-                    if (work) {
-                        trav_record<COUNT>(S, T, cnt);
-                        work = leaf_pending(T);
-                    }
-                }
+            if (tracing) {
+                if (leaf_pending(T))
+                    trav_record<COUNT>(S, T, cnt);
+                else if (T.cur != RT_TRAV_NONE)
+                    trav_node<COUNT, 8, PF>(S, T, stk, g, cnt);
             }
             if (tracing && !leaf_pending(T) && T.cur == RT_TRAV_NONE) {
                 trav_finish(S, T);
@@ -1769,11 +1476,42 @@ __global__ __launch_bounds__(64, WPE) void persistent_df_kernel(KParams P, JobSr
             }
             if (!__any(tracing)) break;
             if (__popcll(__ballot(pending || L.job == -1)) >= refill_at) break;
+            if (P.wave_trace && t_exh) {
+                it_drain++;
+                lanes_drain += (unsigned int)__popcll(__ballot(tracing));
+            }
+            // drain (no lane can take a new job): the remaining queries go to lane groups
+            // (coop 2: also in steady state, for the last queries a full-wave refill waits for)
+            if (COOP && P.coop && ((P.coop == 2 && refill_at == 64) || (!__any(L.job == -1) && __any(L.job == -2)))) {
+                const unsigned long long om = __ballot(tracing);
+                const int k = __popcll(om);
+                if (k <= P.coop_max) {
+                    int G = 64;
+                    while (G > 1 && k * G > 64) G >>= 1;
+                    const int r = __popcll(om & ((1ull << lane_id) - 1ull));
+                    if (tracing) {
+                        coop_put(T, coop_q, r);
+                        int* gp = coop_pool + r * (COOP_POOL * G / 64);
+                        for (int j = 0; j < T.sp; ++j) gp[j] = stk[j * RT_WAVE];
+                        if (T.cur != RT_TRAV_NONE) gp[T.sp] = (int)T.cur;
+                    }
+                    __syncthreads();
+                    const uint2 nv = coop_group_trace<8>(S.nodes, S.tri, S.refn, S.leaf_path, coop_pool, coop_q, om,
+                                                         P.coop_reserve);
+                    __syncthreads();
+                    if (COUNT) {
+                        cnt.nodes += nv.x;
+                        cnt.tris += nv.y;
+                    }
+                    if (tracing) coop_get(T, coop_q, r);
+                    if (P.wave_trace) coop_n++;
+                }
+            }
         }
         if (COUNT) cnt.cyc_b += (unsigned long long)clock64() - tB;
     }
     flush_counters<COUNT>(P, cnt);
-    if (P.wave_trace && lane_id == 0) {  // RT_WAVE_TRACE, 100 MHz clock: start, end, jobs, drain
+    if (P.wave_trace && lane_id == 0) {  // wave trace, 100 MHz clock: start, end, jobs, drain
         unsigned long long* w = P.wave_trace + 8 * blockIdx.x;
         w[0] = t_wave0;
         w[1] = wall_clock64();
@@ -1784,6 +1522,46 @@ __global__ __launch_bounds__(64, WPE) void persistent_df_kernel(KParams P, JobSr
         w[6] = coop_n;
         w[7] = pa_drain;
     }
+}
+
+// BoundingVolumeHierarchy::intersect(ray, hitInfo, useBVH) per ray (rt_intersect): the same
+// trace_query8 and surface() as the renderer.
+__global__ __launch_bounds__(64) void intersect_kernel(DevScene S, const rt_ray* rays, int n, int use_bvh,
+                                                       rt_hit* hits) {
+    __shared__ int stack_lds[RT_STACK_SIZE * RT_WAVE];
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    int* stk = stack_lds + threadIdx.x;
+    if (i >= n) return;
+    const rt_ray r = rays[i];
+    const v3 o{r.origin[0], r.origin[1], r.origin[2]};
+    const v3 d{r.direction[0], r.direction[1], r.direction[2]};
+    Best b;
+    Cnt cnt{};
+    const bool hit = trace_query8<false, 8>(S, o, d, r.t, 0.0f, use_bvh != 0, false, b, stk, cnt);
+    rt_hit h;
+    h.hit = hit ? 1 : 0;
+    h.t = hit ? b.t : r.t;
+    if (hit) {
+        const Surf s = surface(S, o, d, b);
+        h.normal[0] = s.n.x;
+        h.normal[1] = s.n.y;
+        h.normal[2] = s.n.z;
+        h.hit_point[0] = s.p.x;
+        h.hit_point[1] = s.p.y;
+        h.hit_point[2] = s.p.z;
+        h.uv[0] = s.uv.x;
+        h.uv[1] = s.uv.y;
+        h.material_index = s.mesh;
+        h.prim_id = s.prim;
+        h.is_triangle = s.is_tri ? 1 : 0;
+    } else {
+        for (int k = 0; k < 3; ++k) h.normal[k] = h.hit_point[k] = 0.0f;
+        h.uv[0] = h.uv[1] = 0.0f;
+        h.material_index = -1;
+        h.prim_id = -1;
+        h.is_triangle = 0;
+    }
+    hits[i] = h;
 }
 
 }  // namespace rt

@@ -1,6 +1,10 @@
 // rt_runtime.hip -- device context behind the C-ABI: scene upload (once), launches, stats.
 // Replaces BoundingVolumeHierarchy's constructor + renderRayTracing's pixel loop
 // (reference src/bounding_volume_hierarchy.cpp:5-9, src/main.cpp:340-400).
+//
+// One shipped render path per scene-size class: the whole-traversal persistent
+// kernel below 65 536 triangles, the dynamic-fetch persistent kernel above.  Nothing here reads the
+// environment; the developer / test hooks are explicit context options (rt_ctx_set_option).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -17,18 +21,18 @@
 #include "rt_internal.h"
 #include "rt_kernels.hip"
 #include "rt_megakernel.hip"
-#include "rt_wavefront.hip"
-#include "rt_packet.hip"
-#include "rt_schedule.hip"
 
 using namespace rt;
+
+// dynamic-fetch kernel below this many triangles only when forced (RT_OPT_KERNEL): a query on a small
+// scene is a handful of node visits and the per-step refill bookkeeping does not pay (measured on
+// MI355X, DESIGN.md section 6: C1/C2/C5 vs C3/C4)
+#define RT_DF_MIN_TRIANGLES 65536
 
 struct rt_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    DevScene S{};
-    DevScene S8{};  // same scene, nodes/records of the quantised wide BVH (bw > 2)
-    int bw = 8;     // BVH width the persistent kernel walks (fixed at rt_create)
+    DevScene S{};  // quantised BVH8 nodes + triangle records in its leaf order, shading data, lights
     std::vector<void*> allocs;
     unsigned long long* d_stats = nullptr;
     float* d_fb = nullptr;
@@ -36,41 +40,28 @@ struct rt_ctx {
     float* d_img = nullptr;
     size_t img_bytes = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    int nnodes = 0, nrec = 0, ntri = 0;
+    int nnodes = 0, nrec = 0, ntri = 0, nmesh = 0;
     int ref_nodes = 0, ref_levels = 0;
-    int bvh_depth = 0;
-    bool glossy_material = false;  // opaque, ks > 0, shininess != 0 (glossy_ray_count > 1 would call rand())
-    int persistent_blocks[5] = {0, 0, 0, 0, 0};  // resident 64-lane blocks per WPE variant
-    // wavefront path (rt_wavefront.hip): queues, path state, frames, counters
-    float* d_wf_st = nullptr;  // 2 x WF_NFIELDS x cap
-    size_t wf_st_bytes = 0;
-    float* d_wf_res = nullptr;  // res_t[cap] | res_rec[cap]
-    size_t wf_res_bytes = 0;
-    float* d_wf_frames = nullptr;
-    size_t wf_frames_bytes = 0;
-    int* d_wf_cnt = nullptr;  // n[0], n[1], head, pad
-    int* h_wf_cnt = nullptr;  // pinned readback
-    int wf_trace_blocks[5] = {0, 0, 0, 0, 0};
-    std::vector<hipEvent_t> wf_ev;  // trace-launch event pairs
-    // primary packet pass (rt_packet.hip): per-job primary hit
-    float* d_pre = nullptr;  // pre_t[njobs] | pre_rec[njobs]
-    size_t pre_bytes = 0;
     int bvh8_depth = 0;
-    bool df_ok = true;
-    // longest-first schedule (rt_schedule.hip): tile hits | tile offsets | job order
-    float* d_sched = nullptr;
-    size_t sched_bytes = 0;
-    // cost-ordered schedule (RT_SCHED=2): per-job query counts of the previous frame + partition
-    float* d_cost = nullptr;  // cost[njobs] | block hist [16][nblk] | order[njobs]
-    size_t cost_bytes = 0;
-    long long cost_key = -1;  // launch geometry the stored costs belong to
-    // developer wave trace (RT_WAVE_TRACE=1)
+    bool glossy_material = false;  // opaque, ks > 0, shininess != 0 (glossy_ray_count > 1 draws lobes)
+    int persistent_blocks[32] = {0};  // resident 64-lane blocks per (kernel class, variant)
+    // lights (re-uploadable: rt_update_lights)
+    void* d_lights[4] = {nullptr, nullptr, nullptr, nullptr};
+    // developer wave trace (RT_OPT_WAVE_TRACE)
     float* d_wave_trace = nullptr;
     size_t wave_trace_bytes = 0;
     int wave_trace_n = 0;
     // view batch (rt_render_views_device): per-view cameras, 12 floats each
     float* d_views = nullptr;
     size_t views_bytes = 0;
+    // rt_ctx_set_option: test / developer hooks (defaults = the shipped path)
+    int opt_kernel = RT_KERNEL_AUTO;
+    int opt_coop = -1;      // -1: per render shape; 0 off; 1 drain only; 2 drain + full-wave stragglers
+    int opt_coop_max = 0;   // 0: the largest count the LDS pool allows
+    int opt_refill = 0;     // 0: per render shape
+    int opt_wave_trace = 0;
+    int opt_variant = -1;   // -1: the class default (RT_DF_DEFAULT / RT_WT_DEFAULT)
+    char last_kernel[64] = {0};
 };
 
 // Image::Image + initMipmap (src/image.cpp:37-73,408-452): texel k = rgb[k*channels + 0..2] / 255.0f
@@ -111,125 +102,8 @@ static void build_texels(const rt_texture& t, std::vector<float>& out, int& leve
     }
 }
 
-// waves per SIMD the persistent kernel is compiled for (register cap); RT_WPE overrides for A/B runs
-static int wpe() {
-    const char* w = std::getenv("RT_WPE");
-    const int v = w ? std::atoi(w) : 2;
-    return (v == 1 || v == 3 || v == 4) ? v : 2;
-}
-
-// BVH the persistent kernel walks, read once at rt_create: 8 (quantised 8-wide, default),
-// 4 (same node format, 4 slots) or 2 (binary, full-precision boxes); RT_BVH selects for A/B runs
-static int bvh_width_env() {
-    const char* b = std::getenv("RT_BVH");
-    const int v = b ? std::atoi(b) : 8;
-    return (v == 2 || v == 4) ? v : 8;
-}
-
-// RT_KERNEL: "tile" (rt_kernels.hip render_kernel), "persistent" (whole-traversal refill),
-// default: the dynamic-fetch persistent kernel (per-node-visit refill)
-// Default (no RT_KERNEL): whole-traversal refill for small scenes, where a query is a handful of
-// node visits and the per-step refill bookkeeping does not pay; dynamic fetch for large ones
-// (measured on MI355X, DESIGN.md section 6: C1/C2/C5 vs C3/C4).
-static bool use_whole_traversal_kernel(int ntri) {
-    const char* k = std::getenv("RT_KERNEL");
-    if (k && std::strcmp(k, "persistent") == 0) return true;
-    if (k && std::strcmp(k, "df") == 0) return false;
-    return ntri < 65536;
-}
-
-// waiting lanes that end a traversal phase of the dynamic-fetch kernel; RT_REFILL overrides
-// (measured on MI355X, 10 rotated rounds: C3 2.46 / 2.38 / 2.34 ms at 16 / 20 / 24, C4 43.0 ms at all three)
-static int refill_threshold() {
-    const char* r = std::getenv("RT_REFILL");
-    const int v = r ? std::atoi(r) : 24;
-    return std::min(64, std::max(1, v));
-}
-
-// lanes with postponed leaf records that start a leaf phase (64: only when no lane can visit a
-// node); RT_LEAFBATCH overrides
-static int leaf_batch_threshold() {
-    const char* r = std::getenv("RT_LEAFBATCH");
-    const int v = r ? std::atoi(r) : 0;
-    return std::min(64, std::max(0, v));  // 0: if-if (one leaf record or node visit per iteration)
-}
-
-template <bool COUNT, int BW>
-static void launch_wide(int grid, hipStream_t st, const KParams& K, const JobSrc& J, bool df_ok) {
-    if (df_ok && !use_whole_traversal_kernel(K.S.ntri)) {
-        if (wpe() == 1)
-            hipLaunchKernelGGL((persistent_df_kernel<COUNT, 1, BW>), dim3(grid), dim3(64), 0, st, K, J);
-        else if (wpe() == 4)
-            hipLaunchKernelGGL((persistent_df_kernel<COUNT, 4, BW>), dim3(grid), dim3(64), 0, st, K, J);
-        else if (wpe() == 3)
-            hipLaunchKernelGGL((persistent_df_kernel<COUNT, 3, BW>), dim3(grid), dim3(64), 0, st, K, J);
-        else if (!COUNT && !K.S.tex_on)  // production variant: no texture code at all
-            hipLaunchKernelGGL((persistent_df_kernel<false, 2, BW, false>), dim3(grid), dim3(64), 0, st, K, J);
-        else
-            hipLaunchKernelGGL((persistent_df_kernel<COUNT, 2, BW>), dim3(grid), dim3(64), 0, st, K, J);
-        return;
-    }
-    if (wpe() == 1)
-        hipLaunchKernelGGL((persistent_kernel<COUNT, 1, BW>), dim3(grid), dim3(64), 0, st, K, J);
-    else if (!COUNT && !K.S.tex_on && BW == 8)
-        hipLaunchKernelGGL((persistent_kernel<false, 2, 8, false>), dim3(grid), dim3(64), 0, st, K, J);
-    else
-        hipLaunchKernelGGL((persistent_kernel<COUNT, 2, BW>), dim3(grid), dim3(64), 0, st, K, J);
-}
-
-template <bool COUNT>
-static void launch_persistent(int grid, hipStream_t st, KParams K, const JobSrc& J, const rt_ctx* c) {
-    if (c->bw > 2) {
-        K.S = c->S8;
-        if (c->bw == 4)
-            launch_wide<COUNT, 4>(grid, st, K, J, c->df_ok);
-        else
-            launch_wide<COUNT, 8>(grid, st, K, J, c->df_ok);
-    } else {
-        if (wpe() == 1)
-            hipLaunchKernelGGL((persistent_kernel<COUNT, 1, 2>), dim3(grid), dim3(64), 0, st, K, J);
-        else
-            hipLaunchKernelGGL((persistent_kernel<COUNT, 2, 2>), dim3(grid), dim3(64), 0, st, K, J);
-    }
-}
-
-static int persistent_grid(rt_ctx* c) {
-    if (const char* g = std::getenv("RT_GRID")) {  // A/B override: blocks per CU
-        int cus = 0;
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
-        return std::max(1, cus) * std::max(1, std::atoi(g));
-    }
-    if (c->persistent_blocks[wpe()] > 0) return c->persistent_blocks[wpe()];
-    int cus = 0, per_cu = 0;
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
-    hipError_t e = hipErrorInvalidValue;
-    // every BVH width compiles to the same LDS footprint and register cap per WPE
-    if (wpe() == 1)
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_df_kernel<false, 1, 8>, 64, 0);
-    else if (wpe() == 3)
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_df_kernel<false, 3, 8>, 64, 0);
-    else if (wpe() == 4)
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_df_kernel<false, 4, 8>, 64, 0);
-    else
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_df_kernel<false, 2, 8>, 64, 0);
-    if (e != hipSuccess || per_cu <= 0) per_cu = 8;
-    c->persistent_blocks[wpe()] = std::max(1, cus) * per_cu;
-    return c->persistent_blocks[wpe()];
-}
-
 // d_stats: 16 counters, then the 8 per-XCD job heads (128-B apart) of the dynamic-fetch kernel
 #define RT_STATS_BYTES ((16 + 8 * 16) * sizeof(unsigned long long))
-
-// per-XCD job ranges for the dynamic-fetch kernel (RT_XCD=0: one global job counter)
-static bool use_xcd_queues() {
-    const char* x = std::getenv("RT_XCD");
-    return !(x && x[0] == '0');
-}
-
-static bool use_tile_kernel() {
-    const char* k = std::getenv("RT_KERNEL");
-    return k && std::strcmp(k, "tile") == 0;
-}
 
 #define HIP_TRY(expr)                                                                           \
     do {                                                                                        \
@@ -262,26 +136,30 @@ static int upload_bytes(rt_ctx* c, const void* host, size_t bytes, void** dev_ou
         dst = reinterpret_cast<decltype(dst)>(p_);                                     \
     } while (0)
 
+
+static int ensure(rt_ctx* c, float** buf, size_t* cap, size_t bytes) {
+    if (*cap >= bytes) return RT_OK;
+    if (*buf) hipFree(*buf);
+    *buf = nullptr;
+    *cap = 0;
+    HIP_TRY(hipMalloc((void**)buf, bytes));
+    *cap = bytes;
+    return RT_OK;
+}
+
 extern "C" int rt_destroy(rt_ctx* c) {
     if (!c) return RT_OK;
     hipSetDevice(c->device);
     for (void* p : c->allocs) hipFree(p);
+    for (void* p : c->d_lights)
+        if (p) hipFree(p);
     if (c->d_stats) hipFree(c->d_stats);
     if (c->d_fb) hipFree(c->d_fb);
     if (c->d_img) hipFree(c->d_img);
     if (c->ev0) hipEventDestroy(c->ev0);
     if (c->ev1) hipEventDestroy(c->ev1);
-    if (c->d_wf_st) hipFree(c->d_wf_st);
-    if (c->d_wf_res) hipFree(c->d_wf_res);
-    if (c->d_wf_frames) hipFree(c->d_wf_frames);
-    if (c->d_wf_cnt) hipFree(c->d_wf_cnt);
-    if (c->d_pre) hipFree(c->d_pre);
     if (c->d_wave_trace) hipFree(c->d_wave_trace);
     if (c->d_views) hipFree(c->d_views);
-    if (c->d_sched) hipFree(c->d_sched);
-    if (c->d_cost) hipFree(c->d_cost);
-    if (c->h_wf_cnt) hipHostFree(c->h_wf_cnt);
-    for (hipEvent_t e : c->wf_ev) hipEventDestroy(e);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
     return RT_OK;
@@ -310,6 +188,72 @@ extern "C" int rt_device_count(int* n) {
     return RT_OK;
 }
 
+// Materials of the meshes and spheres as the kernels read them (+ the glossy lobe width), and the
+// scene-wide flags they imply.
+static void device_materials(const rt_material* mm, int nmesh, std::vector<DMat>& mats, bool& all_opaque,
+                             bool& glossy) {
+    mats.assign(nmesh, DMat{});
+    for (int m = 0; m < nmesh; ++m) {
+        const rt_material& sm = mm[m];
+        for (int k = 0; k < 3; ++k) {
+            mats[m].kd[k] = sm.kd[k];
+            mats[m].ks[k] = sm.ks[k];
+        }
+        mats[m].shin = sm.shininess;
+        mats[m].transp = sm.transparency;
+        mats[m].gd = glossy_width(sm.shininess);
+        if (sm.transparency != 1.0f) all_opaque = false;
+        if (sm.transparency == 1.0f && (sm.ks[0] > 0 || sm.ks[1] > 0 || sm.ks[2] > 0) && sm.shininess != 0.0f)
+            glossy = true;
+    }
+}
+
+static DMat device_material(const rt_material& sm, bool& all_opaque, bool& glossy) {
+    std::vector<DMat> one;
+    device_materials(&sm, 1, one, all_opaque, glossy);
+    return one[0];
+}
+
+// (Re-)upload the four light arrays (getPointLights & co. read them, src/shadow.cpp:106-321).
+static int upload_lights(rt_ctx* c, const rt_scene_desc* d) {
+    std::vector<DSpot> spots(d->num_spot_lights);
+    for (int i = 0; i < d->num_spot_lights; ++i) {
+        const rt_spot_light& L = d->spot_lights[i];
+        for (int k = 0; k < 3; ++k) {
+            spots[i].pos[k] = L.position[k];
+            spots[i].dir[k] = L.direction[k];
+            spots[i].color[k] = L.color[k];
+        }
+        // std::cos(glm::radians(light.angle)) (src/shadow.cpp:235)
+        spots[i].cos_angle = std::cos(L.angle * static_cast<float>(0.01745329251994329576923690768489));
+    }
+    const void* src[4] = {d->point_lights, d->spherical_lights, spots.data(), d->plane_lights};
+    const size_t bytes[4] = {(size_t)d->num_point_lights * sizeof(rt_point_light),
+                             (size_t)d->num_spherical_lights * sizeof(rt_spherical_light),
+                             spots.size() * sizeof(DSpot), (size_t)d->num_plane_lights * sizeof(rt_plane_light)};
+    for (int k = 0; k < 4; ++k) {
+        if (c->d_lights[k]) hipFree(c->d_lights[k]);
+        c->d_lights[k] = nullptr;
+        if (bytes[k] == 0) continue;
+        if (!src[k]) {
+            set_error("light array is null but its count is not 0");
+            return RT_ERR_INVALID;
+        }
+        HIP_TRY(hipMalloc(&c->d_lights[k], bytes[k]));
+        HIP_TRY(hipMemcpy(c->d_lights[k], src[k], bytes[k], hipMemcpyHostToDevice));
+    }
+    DevScene& S = c->S;
+    S.pl = static_cast<const rt_point_light*>(c->d_lights[0]);
+    S.sl = static_cast<const rt_spherical_light*>(c->d_lights[1]);
+    S.spot = static_cast<const DSpot*>(c->d_lights[2]);
+    S.plane = static_cast<const rt_plane_light*>(c->d_lights[3]);
+    S.npl = d->num_point_lights;
+    S.nsl = d->num_spherical_lights;
+    S.nspot = d->num_spot_lights;
+    S.nplane = d->num_plane_lights;
+    return RT_OK;
+}
+
 extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
     if (!desc || !out) {
         set_error("rt_create: null argument");
@@ -330,7 +274,8 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
     const int ntri = desc->num_triangles;
     if (ntri < 0 || (ntri > 0 && (!desc->positions || !desc->normals || !desc->mesh_index)) ||
         desc->num_meshes < 0 || (ntri > 0 && !desc->materials) || desc->num_spheres < 0 ||
-        (desc->num_spheres > 0 && !desc->spheres)) {
+        (desc->num_spheres > 0 && !desc->spheres) || desc->num_point_lights < 0 || desc->num_spherical_lights < 0 ||
+        desc->num_spot_lights < 0 || desc->num_plane_lights < 0 || desc->num_textures < 0) {
         set_error("rt_create: invalid scene description");
         return RT_ERR_INVALID;
     }
@@ -347,6 +292,7 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
         return RT_ERR_HIP;
     }
     c->ntri = ntri;
+    c->nmesh = desc->num_meshes;
 
     // --- reference BVH (object order: triangles, then spheres) ---
     std::vector<float> sph4(desc->num_spheres * 4);
@@ -354,7 +300,14 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
         for (int k = 0; k < 3; ++k) sph4[s * 4 + k] = desc->spheres[s].center[k];
         sph4[s * 4 + 3] = desc->spheres[s].radius;
     }
-    RefBvh ref = build_ref_bvh(desc->positions, ntri, sph4.data(), desc->num_spheres, 4);
+    RefBvh ref;
+    try {
+        ref = build_ref_bvh(desc->positions, ntri, sph4.data(), desc->num_spheres, 4);
+    } catch (const std::exception& ex) {
+        set_error(std::string("rt_create: ") + ex.what());
+        delete c;
+        return RT_ERR_INVALID;
+    }
     c->ref_nodes = (int)ref.nodes.size();
     c->ref_levels = ref.max_level_achieved + 1;
     if (c->ref_nodes > RT_MAX_REF_NODES) {
@@ -377,116 +330,60 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
         for (size_t k = 0; k < ref.leaf_path[l].size(); ++k) leaf_path[l * 8 + 1 + k] = ref.leaf_path[l][k];
     }
 
-    // --- BVH2 over triangles, boxes inflated by eps (see DESIGN.md "conservative traversal") ---
+    // --- binned-SAH BVH2 (boxes inflated by eps, DESIGN.md "conservative traversal") collapsed into
+    // the quantised BVH8 the kernels walk ---
     float max_abs = 8.0f;
     for (size_t i = 0; i < (size_t)ntri * 9; ++i) max_abs = std::max(max_abs, std::fabs(desc->positions[i]));
     const float eps = std::ldexp(max_abs, -16);
-    Bvh2 bvh = build_bvh2(desc->positions, ntri, eps, 4);
-    c->bvh_depth = bvh.max_depth;
-    if (bvh.max_depth + 2 >= RT_STACK_SIZE) {
-        set_error("rt_create: BVH deeper than the traversal stack");
-        delete c;
-        return RT_ERR_INVALID;
-    }
-    c->nnodes = (int)bvh.nodes.size();
-    c->nrec = ntri;
-
-    // --- triangle records (64 B): v0|n.x, v1|n.y, v2|n.z, D|key_brute|key_bvh|ref_leaf ---
-    auto make_records = [&](const std::vector<int>& order) {
-        std::vector<float> rec((size_t)ntri * 16);
-        for (int r = 0; r < ntri; ++r) {
-            const int t = order[r];
-            const float* p = desc->positions + (size_t)t * 9;
-            const v3 v0{p[0], p[1], p[2]}, v1{p[3], p[4], p[5]}, v2{p[6], p[7], p[8]};
-            // trianglePlane (src/ray_tracing.cpp:91-100)
-            const v3 n = normalize(cross(v0 - v2, v1 - v2));
-            const float D = dot(n, v0);
-            float* o = rec.data() + (size_t)r * 16;
-            o[0] = v0.x; o[1] = v0.y; o[2] = v0.z; o[3] = n.x;
-            o[4] = v1.x; o[5] = v1.y; o[6] = v1.z; o[7] = n.y;
-            o[8] = v2.x; o[9] = v2.y; o[10] = v2.z; o[11] = n.z;
-            int ib[4] = {0, t, ref.tri_key[t], ref.tri_leaf[t]};
-            std::memcpy(&o[12], &D, 4);
-            std::memcpy(&o[13], &ib[1], 12);
-        }
-        return rec;
-    };
-    const std::vector<float> rec = make_records(bvh.order);
-    c->bw = bvh_width_env();
     Bvh8 bvh8;
     try {
-        if (c->bw > 2) bvh8 = build_bvh8(bvh, c->bw);
+        const Bvh2 bvh = build_bvh2(desc->positions, ntri, eps, 4);
+        bvh8 = build_bvh8(bvh, 8);
     } catch (const std::exception& ex) {
         set_error(std::string("rt_create: ") + ex.what());
         delete c;
         return RT_ERR_INVALID;
     }
     c->bvh8_depth = bvh8.max_depth;
-    c->df_ok = bvh8.max_depth + 2 < RT_STACK8;  // the dynamic-fetch kernel's smaller LDS stack
-    if (c->bw > 2 && (bvh8.max_depth + 2 >= RT_STACK_SIZE || (int)bvh8.order.size() != ntri)) {
+    if (bvh8.max_depth + 2 >= RT_STACK8 || (int)bvh8.order.size() != ntri) {
         set_error("rt_create: BVH8 deeper than the traversal stack");
         delete c;
         return RT_ERR_INVALID;
     }
-    const std::vector<float> rec8 = c->bw > 2 ? make_records(bvh8.order) : std::vector<float>();
-    std::vector<float> nodes((size_t)bvh.nodes.size() * 16);
-    for (size_t i = 0; i < bvh.nodes.size(); ++i) {
-        const Bvh2Node& nd = bvh.nodes[i];
-        float* o = nodes.data() + i * 16;
-        o[0] = nd.lo0[0]; o[1] = nd.lo0[1]; o[2] = nd.lo0[2]; o[3] = nd.hi0[0];
-        o[4] = nd.hi0[1]; o[5] = nd.hi0[2]; o[6] = nd.lo1[0]; o[7] = nd.lo1[1];
-        o[8] = nd.lo1[2]; o[9] = nd.hi1[0]; o[10] = nd.hi1[1]; o[11] = nd.hi1[2];
-        std::memcpy(&o[12], &nd.child[0], 4);
-        std::memcpy(&o[13], &nd.child[1], 4);
-        std::memcpy(&o[14], &nd.count[0], 4);
-        std::memcpy(&o[15], &nd.count[1], 4);
+    c->nnodes = (int)(bvh8.nodes.size() / 32);
+    c->nrec = ntri;
+
+    // --- triangle records (64 B) in BVH8 leaf order: v0|n.x, v1|n.y, v2|n.z, D|key_brute|key_bvh|ref_leaf ---
+    std::vector<float> rec((size_t)ntri * 16);
+    for (int r = 0; r < ntri; ++r) {
+        const int t = bvh8.order[r];
+        const float* p = desc->positions + (size_t)t * 9;
+        const v3 v0{p[0], p[1], p[2]}, v1{p[3], p[4], p[5]}, v2{p[6], p[7], p[8]};
+        // trianglePlane (src/ray_tracing.cpp:91-100)
+        const v3 n = normalize(cross(v0 - v2, v1 - v2));
+        const float D = dot(n, v0);
+        float* o = rec.data() + (size_t)r * 16;
+        o[0] = v0.x; o[1] = v0.y; o[2] = v0.z; o[3] = n.x;
+        o[4] = v1.x; o[5] = v1.y; o[6] = v1.z; o[7] = n.y;
+        o[8] = v2.x; o[9] = v2.y; o[10] = v2.z; o[11] = n.z;
+        int ib[3] = {t, ref.tri_key[t], ref.tri_leaf[t]};
+        std::memcpy(&o[12], &D, 4);
+        std::memcpy(&o[13], ib, 12);
     }
 
-    std::vector<DMat> mats(desc->num_meshes);
-    bool all_opaque = true;
-    for (int m = 0; m < desc->num_meshes; ++m) {
-        const rt_material& sm = desc->materials[m];
-        for (int k = 0; k < 3; ++k) {
-            mats[m].kd[k] = sm.kd[k];
-            mats[m].ks[k] = sm.ks[k];
-        }
-        mats[m].shin = sm.shininess;
-        mats[m].transp = sm.transparency;
-        mats[m].gd = glossy_width(sm.shininess);
-        if (sm.transparency != 1.0f) all_opaque = false;
-        if (sm.transparency == 1.0f && (sm.ks[0] > 0 || sm.ks[1] > 0 || sm.ks[2] > 0) && sm.shininess != 0.0f)
-            c->glossy_material = true;
-    }
+    bool all_opaque = true, glossy = false;
+    std::vector<DMat> mats;
+    device_materials(desc->materials, desc->num_meshes, mats, all_opaque, glossy);
     std::vector<DSph> sph(desc->num_spheres);
     for (int s = 0; s < desc->num_spheres; ++s) {
         const rt_sphere& ss = desc->spheres[s];
-        for (int k = 0; k < 3; ++k) {
-            sph[s].c[k] = ss.center[k];
-            sph[s].m.kd[k] = ss.material.kd[k];
-            sph[s].m.ks[k] = ss.material.ks[k];
-        }
+        for (int k = 0; k < 3; ++k) sph[s].c[k] = ss.center[k];
         sph[s].r = ss.radius;
-        sph[s].m.shin = ss.material.shininess;
-        sph[s].m.transp = ss.material.transparency;
-        sph[s].m.gd = glossy_width(ss.material.shininess);
+        sph[s].m = device_material(ss.material, all_opaque, glossy);
         sph[s].key_bvh = ref.sph_key[s];
         sph[s].leaf = ref.sph_leaf[s];
-        if (ss.material.transparency != 1.0f) all_opaque = false;
-        const rt_material& sm = ss.material;
-        if (sm.transparency == 1.0f && (sm.ks[0] > 0 || sm.ks[1] > 0 || sm.ks[2] > 0) && sm.shininess != 0.0f)
-            c->glossy_material = true;
     }
-    std::vector<DSpot> spots(desc->num_spot_lights);
-    for (int i = 0; i < desc->num_spot_lights; ++i) {
-        const rt_spot_light& L = desc->spot_lights[i];
-        for (int k = 0; k < 3; ++k) {
-            spots[i].pos[k] = L.position[k];
-            spots[i].dir[k] = L.direction[k];
-            spots[i].color[k] = L.color[k];
-        }
-        // std::cos(glm::radians(light.angle)) (src/shadow.cpp:235)
-        spots[i].cos_angle = std::cos(L.angle * static_cast<float>(0.01745329251994329576923690768489));
-    }
+    c->glossy_material = glossy;
 
     // kd textures: texels and mip chains (built here, once), per-mesh texture index
     std::vector<float> texels;
@@ -517,12 +414,8 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
     }
 
     DevScene& S = c->S;
-    const float4* d_rec = nullptr;
-    const float4* d_nodes = nullptr;
-    UP(reinterpret_cast<const float4*>(rec.data()), (size_t)ntri * 4, d_rec);
-    UP(reinterpret_cast<const float4*>(nodes.data()), bvh.nodes.size() * 4, d_nodes);
-    S.tri = d_rec;
-    S.nodes = d_nodes;
+    UP(reinterpret_cast<const float4*>(rec.data()), (size_t)ntri * 4, S.tri);
+    UP(reinterpret_cast<const float4*>(bvh8.nodes.data()), bvh8.nodes.size() / 4, S.nodes);
     std::vector<float> uvz;
     const float* uvp = desc->texcoords;
     if (!uvp) {
@@ -536,10 +429,6 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
     UP(sph.data(), sph.size(), S.sph);
     UP(refn.data(), refn.size(), S.refn);
     UP(leaf_path.data(), leaf_path.size(), S.leaf_path);
-    UP(desc->point_lights, (size_t)desc->num_point_lights, S.pl);
-    UP(desc->spherical_lights, (size_t)desc->num_spherical_lights, S.sl);
-    UP(spots.data(), spots.size(), S.spot);
-    UP(desc->plane_lights, (size_t)desc->num_plane_lights, S.plane);
     UP(texels.data(), texels.size(), S.tex);
     UP(tex_info.data(), tex_info.size(), S.tex_info);
     UP(mat_tex.data(), mat_tex.size(), S.mat_tex);
@@ -547,21 +436,12 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
     S.ntri = ntri;
     S.nsph = desc->num_spheres;
     S.nref = (int)refn.size();
-    S.npl = desc->num_point_lights;
-    S.nsl = desc->num_spherical_lights;
-    S.nspot = desc->num_spot_lights;
-    S.nplane = desc->num_plane_lights;
     S.all_opaque = all_opaque ? 1 : 0;
-
-    // 8-wide variant: same scene, records permuted into the BVH8 leaf order
-    c->S8 = S;
-    const float4* d_rec8 = nullptr;
-    const float4* d_nodes8 = nullptr;
-    UP(reinterpret_cast<const float4*>(rec8.data()), rec8.size() / 4, d_rec8);
-    UP(reinterpret_cast<const float4*>(bvh8.nodes.data()), bvh8.nodes.size() / 4, d_nodes8);
-    c->S8.tri = d_rec8;
-    c->S8.nodes = d_nodes8;
-
+    int rc = upload_lights(c, desc);
+    if (rc != RT_OK) {
+        rt_destroy(c);
+        return rc;
+    }
     if (hipMalloc(&c->d_stats, RT_STATS_BYTES) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
@@ -571,6 +451,183 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
     }
     *out = c;
     return RT_OK;
+}
+
+// ImGui light edits after the BVH exists (src/main.cpp:511-613): the light arrays of `desc` replace
+// the context's; geometry, materials and textures are untouched, nothing is rebuilt.
+extern "C" int rt_update_lights(rt_ctx* c, const rt_scene_desc* desc) {
+    if (!c || !desc || desc->num_point_lights < 0 || desc->num_spherical_lights < 0 || desc->num_spot_lights < 0 ||
+        desc->num_plane_lights < 0) {
+        set_error("rt_update_lights: invalid argument");
+        return RT_ERR_INVALID;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return upload_lights(c, desc);
+}
+
+// Material edits (kd, ks, shininess, transparency of a mesh or a sphere) after the BVH exists: the
+// reference's BVH and shadow culling do not depend on materials, so nothing is rebuilt.
+extern "C" int rt_update_materials(rt_ctx* c, int num_meshes, const rt_material* materials, int num_spheres,
+                                   const rt_material* sphere_materials) {
+    if (!c || num_meshes != c->nmesh || num_spheres != c->S.nsph || (num_meshes > 0 && !materials) ||
+        (num_spheres > 0 && !sphere_materials)) {
+        set_error("rt_update_materials: counts must match the context's meshes and spheres");
+        return RT_ERR_INVALID;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    bool all_opaque = true, glossy = false;
+    std::vector<DMat> mats;
+    device_materials(materials, num_meshes, mats, all_opaque, glossy);
+    std::vector<DSph> sph(num_spheres);
+    if (num_spheres > 0)
+        HIP_TRY(hipMemcpy(sph.data(), c->S.sph, sph.size() * sizeof(DSph), hipMemcpyDeviceToHost));
+    for (int s = 0; s < num_spheres; ++s) sph[s].m = device_material(sphere_materials[s], all_opaque, glossy);
+    if (!mats.empty())
+        HIP_TRY(hipMemcpy(const_cast<DMat*>(c->S.mats), mats.data(), mats.size() * sizeof(DMat), hipMemcpyHostToDevice));
+    if (!sph.empty())
+        HIP_TRY(hipMemcpy(const_cast<DSph*>(c->S.sph), sph.data(), sph.size() * sizeof(DSph), hipMemcpyHostToDevice));
+    c->S.all_opaque = all_opaque ? 1 : 0;
+    c->glossy_material = glossy;
+    for (int m = 0; m < num_meshes; ++m)  // a texture binding cannot change here (textures are uploaded once)
+        (void)m;
+    return RT_OK;
+}
+
+extern "C" int rt_ctx_set_option(rt_ctx* c, int option, int value) {
+    if (!c) {
+        set_error("rt_ctx_set_option: null ctx");
+        return RT_ERR_INVALID;
+    }
+    switch (option) {
+        case RT_OPT_KERNEL:
+            if (value < RT_KERNEL_AUTO || value > RT_KERNEL_DYNAMIC_FETCH) break;
+            if (value == RT_KERNEL_DYNAMIC_FETCH && c->bvh8_depth + 2 >= RT_STACK8) {
+                set_error("rt_ctx_set_option: BVH8 too deep for the dynamic-fetch kernel's stack");
+                return RT_ERR_INVALID;
+            }
+            c->opt_kernel = value;
+            return RT_OK;
+        case RT_OPT_COOP:
+            if (value < -1 || value > 2) break;
+            c->opt_coop = value;
+            return RT_OK;
+        case RT_OPT_COOP_MAX:
+            if (value < 0 || value > COOP_Q) break;
+            c->opt_coop_max = value;
+            return RT_OK;
+        case RT_OPT_REFILL:
+            if (value < 0 || value > 64) break;
+            c->opt_refill = value;
+            return RT_OK;
+        case RT_OPT_WAVE_TRACE:
+            c->opt_wave_trace = value ? 1 : 0;
+            return RT_OK;
+        case RT_OPT_VARIANT:
+            if (value < -1 || value > 15) break;
+            c->opt_variant = value;
+            return RT_OK;
+        default:
+            set_error("rt_ctx_set_option: unknown option");
+            return RT_ERR_INVALID;
+    }
+    set_error("rt_ctx_set_option: value out of range");
+    return RT_ERR_INVALID;
+}
+
+
+// the kernel class a render runs: whole-traversal refill for small scenes, dynamic fetch for large
+static bool use_df(const rt_ctx* c) {
+    if (c->opt_kernel == RT_KERNEL_WHOLE_TRAVERSAL) return false;
+    if (c->opt_kernel == RT_KERNEL_DYNAMIC_FETCH) return true;
+    return c->ntri >= RT_DF_MIN_TRIANGLES;
+}
+
+// Kernel variants compiled (rt_megakernel.hip RT_V_*): the shipped default of each class first, then
+// the alternatives kept for A/B measurement (RT_OPT_VARIANT; all render identical bits).
+#define RT_DF_DEFAULT (RT_V_CALL | RT_V_NOPF)
+#define RT_WT_DEFAULT (RT_V_CALL | RT_V_W3)
+static const int kDfVariants[] = {RT_DF_DEFAULT, 0, RT_V_CALL, RT_V_CALL | RT_V_NOPF | RT_V_NOCOOP | RT_V_W3};
+static const int kWtVariants[] = {RT_WT_DEFAULT, 0};
+
+static int variant_of(const rt_ctx* c, bool df) {
+    if (c->opt_variant >= 0) return c->opt_variant;
+    return df ? RT_DF_DEFAULT : RT_WT_DEFAULT;
+}
+
+template <bool COUNT, bool TEX, int V>
+static void launch_v(bool df, int grid, hipStream_t st, const KParams& K, const JobSrc& J) {
+    if (df)
+        hipLaunchKernelGGL((persistent_df_kernel<COUNT, TEX, V>), dim3(grid), dim3(64), 0, st, K, J);
+    else
+        hipLaunchKernelGGL((persistent_kernel<COUNT, TEX, V>), dim3(grid), dim3(64), 0, st, K, J);
+}
+
+template <bool COUNT>
+static int launch_persistent(int grid, hipStream_t st, const KParams& K, const JobSrc& J, rt_ctx* c) {
+    const bool df = use_df(c);
+    const bool tex = COUNT || K.S.tex_on;  // counting builds keep the texture code (one instance each)
+    const int v = variant_of(c, df);
+    const int dv = df ? RT_DF_DEFAULT : RT_WT_DEFAULT;
+    if (COUNT || tex) {
+        if (v != dv) {
+            set_error("kernel variant: counting and textured renders exist in the default variant only");
+            return RT_ERR_INVALID;
+        }
+        if (df) launch_v<COUNT, true, RT_DF_DEFAULT>(true, grid, st, K, J);
+        else launch_v<COUNT, true, RT_WT_DEFAULT>(false, grid, st, K, J);
+    } else if (df) {
+        switch (v) {
+            case RT_DF_DEFAULT: launch_v<false, false, RT_DF_DEFAULT>(true, grid, st, K, J); break;
+            case 0: launch_v<false, false, 0>(true, grid, st, K, J); break;
+            case RT_V_CALL: launch_v<false, false, RT_V_CALL>(true, grid, st, K, J); break;
+            case RT_V_CALL | RT_V_NOPF | RT_V_NOCOOP | RT_V_W3:
+                launch_v<false, false, RT_V_CALL | RT_V_NOPF | RT_V_NOCOOP | RT_V_W3>(true, grid, st, K, J);
+                break;
+            default: set_error("kernel variant not compiled"); return RT_ERR_INVALID;
+        }
+    } else {
+        switch (v) {
+            case RT_WT_DEFAULT: launch_v<false, false, RT_WT_DEFAULT>(false, grid, st, K, J); break;
+            case 0: launch_v<false, false, 0>(false, grid, st, K, J); break;
+            default: set_error("kernel variant not compiled"); return RT_ERR_INVALID;
+        }
+    }
+    // the name rocprofv3 lists for this launch (bench.py's roofline.kernel)
+    std::snprintf(c->last_kernel, sizeof(c->last_kernel), "rt::%s<%s, %s, %d>",
+                  df ? "persistent_df_kernel" : "persistent_kernel", COUNT ? "true" : "false", tex ? "true" : "false",
+                  v);
+    return RT_OK;
+}
+
+template <bool DF, int V>
+static int occupancy_of(int* per_cu) {
+    if (DF) return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, persistent_df_kernel<false, false, V>, 64, 0);
+    return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, persistent_kernel<false, false, V>, 64, 0);
+}
+
+// resident 64-lane blocks of the kernel (the persistent grid)
+static int persistent_grid(rt_ctx* c) {
+    const bool df = use_df(c);
+    const int v = variant_of(c, df);
+    const int key = (df ? 16 : 0) + (v & 15);
+    if (c->persistent_blocks[key] > 0) return c->persistent_blocks[key];
+    int cus = 0, per_cu = 0;
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
+    int e = 1;
+    if (df) {
+        if (v == RT_DF_DEFAULT) e = occupancy_of<true, RT_DF_DEFAULT>(&per_cu);
+        else if (v == 0) e = occupancy_of<true, 0>(&per_cu);
+        else if (v == RT_V_CALL) e = occupancy_of<true, RT_V_CALL>(&per_cu);
+        else e = occupancy_of<true, RT_V_CALL | RT_V_NOPF | RT_V_NOCOOP | RT_V_W3>(&per_cu);
+    } else {
+        if (v == RT_WT_DEFAULT) e = occupancy_of<false, RT_WT_DEFAULT>(&per_cu);
+        else e = occupancy_of<false, 0>(&per_cu);
+    }
+    if (e != 0 || per_cu <= 0) per_cu = 8;
+    c->persistent_blocks[key] = std::max(1, cus) * per_cu;
+    return c->persistent_blocks[key];
 }
 
 static int fill_params(rt_ctx* c, const rt_camera* cam, const rt_params* p, int W, int H, KParams& K) {
@@ -586,12 +643,16 @@ static int fill_params(rt_ctx* c, const rt_camera* cam, const rt_params* p, int 
         set_error("glossy_ray_count must be >= 1");
         return RT_ERR_INVALID;
     }
-    if (p->glossy_ray_count != 1 && c->glossy_material && p->max_reflection_level > 0 && use_tile_kernel()) {
-        set_error("glossy_ray_count > 1: the tile kernel has no glossy lobes (use the persistent kernels)");
-        return RT_ERR_INVALID;
-    }
     if (p->multiple_rays && !(p->sample_size == 4 || p->sample_size == 16 || p->sample_size == 64)) {
         set_error("sample_size must be 4, 16 or 64");
+        return RT_ERR_INVALID;
+    }
+    if (p->sphere_light_ray_count < 2 && c->S.nsl > 0) {
+        set_error("sphere_light_ray_count must be >= 2 (getSpherelights divides by (count - 1) / m)");
+        return RT_ERR_INVALID;
+    }
+    if (p->plane_light_1D_ray_count < 2 && c->S.nplane > 0) {
+        set_error("plane_light_1D_ray_count must be >= 2 (getPlaneLights divides by k - 1)");
         return RT_ERR_INVALID;
     }
     if (p->texture_filtering < RT_TEX_NEAREST || p->texture_filtering > RT_TEX_TRILINEAR ||
@@ -600,16 +661,18 @@ static int fill_params(rt_ctx* c, const rt_camera* cam, const rt_params* p, int 
         set_error("texture_filtering / out_of_bounds rule out of range");
         return RT_ERR_INVALID;
     }
-    std::memset(&K, 0, sizeof(K));
-    // per-render texture state (useTextures, textureFiltering, out-of-bounds rules, border colour)
-    for (DevScene* sc : {&c->S, &c->S8}) {
-        sc->tex_on = (p->use_textures && c->S.ntex > 0) ? 1 : 0;
-        sc->tex_filter = p->texture_filtering;
-        sc->tex_oob_x = p->out_of_bounds_x;
-        sc->tex_oob_y = p->out_of_bounds_y;
-        for (int k = 0; k < 3; ++k) sc->tex_border[k] = p->border_color[k];
+    if ((size_t)W * (size_t)H >= (size_t)1 << 32) {
+        set_error("image too large (pixel ids are 32-bit)");
+        return RT_ERR_INVALID;
     }
+    std::memset(&K, 0, sizeof(K));
     K.S = c->S;
+    // per-render texture state (useTextures, textureFiltering, out-of-bounds rules, border colour)
+    K.S.tex_on = (p->use_textures && c->S.ntex > 0) ? 1 : 0;
+    K.S.tex_filter = p->texture_filtering;
+    K.S.tex_oob_x = p->out_of_bounds_x;
+    K.S.tex_oob_y = p->out_of_bounds_y;
+    for (int k = 0; k < 3; ++k) K.S.tex_border[k] = p->border_color[k];
     K.max_level = p->max_reflection_level;
     K.glossy_n = p->glossy_ray_count;
     K.seed_lo = (uint32_t)(p->rng_seed & 0xFFFFFFFFull);
@@ -618,9 +681,9 @@ static int fill_params(rt_ctx* c, const rt_camera* cam, const rt_params* p, int 
     K.use_bvh = p->use_bvh ? 1 : 0;
     K.refr = p->refraction_factor;
     // getSpherelights ring/spoke counts (src/shadow.cpp:190-195), host float math as the reference
-    const int rc = p->sphere_light_ray_count;
+    const int rc = std::max(2, p->sphere_light_ray_count);
     const int m = std::max(1, (int)(rc / std::round(std::sqrt(2 * 3.14159365358979f * rc))));
-    const int n = (rc - 1) / m;
+    const int n = std::max(1, (rc - 1) / m);
     K.sl_m = m;
     K.sl_n = n;
     K.sl_count = m * n + 1;
@@ -650,395 +713,82 @@ static int fill_params(rt_ctx* c, const rt_camera* cam, const rt_params* p, int 
     K.aa_offx = 1.0f / (float)W * 0.25f;
     K.aa_offy = 1.0f / (float)H * 0.25f;
     K.stats = c->d_stats;
-    K.refill = refill_threshold();
-    {
-        const char* cp = std::getenv("RT_COOP");  // drain-phase cooperative traversal (default on)
-        K.coop = (cp && cp[0] == '0') ? 0 : ((cp && cp[0] == '2') ? 2 : 1);
-        // a group of G lanes owns COOP_POOL * G / 64 pool slots: the depth-first reserve plus one
-        // breadth step must fit; coop_max = the largest query count whose groups still do
-        K.coop_reserve = 7 * (c->bvh8_depth + 1) + 8;
-        K.coop_max = 0;
-        for (int k = 1; k <= COOP_Q; ++k) {
-            int G = 64;
-            while (G > 1 && k * G > 64) G >>= 1;
-            if (COOP_POOL * G / 64 >= K.coop_reserve + 8 * G) K.coop_max = k;
-        }
-        if (const char* cm = std::getenv("RT_COOP_MAX")) K.coop_max = std::min(K.coop_max, std::atoi(cm));
-        if (K.coop_max <= 0) K.coop = 0;
+    // dynamic-fetch refill and drain lane groups, by render shape: a single
+    // frame with sample-heavy lights (spherical / plane) advances at 24 waiting lanes; frames with few
+    // shadow samples per shading point and view batches advance whole waves (64), and hand the last
+    // queries a full-wave refill waits for to lane groups (coop 2)
+    const bool few_samples = K.S.nsl * K.sl_count + K.S.nplane * K.plane_k * K.plane_k <= 4;
+    K.refill = few_samples ? 64 : 24;
+    K.coop = few_samples ? 2 : 1;
+    // a group of G lanes owns COOP_POOL * G / 64 pool slots: the depth-first reserve plus one breadth
+    // step must fit; coop_max = the largest query count whose groups still do
+    K.coop_reserve = 7 * (c->bvh8_depth + 1) + 8;
+    K.coop_max = 0;
+    for (int k = 1; k <= COOP_Q; ++k) {
+        int G = 64;
+        while (G > 1 && k * G > 64) G >>= 1;
+        if (COOP_POOL * G / 64 >= K.coop_reserve + 8 * G) K.coop_max = k;
     }
-    K.leaf_batch = leaf_batch_threshold();
     return RT_OK;
 }
 
-static int ensure(rt_ctx* c, float** buf, size_t* cap, size_t bytes) {
-    if (*cap >= bytes) return RT_OK;
-    if (*buf) hipFree(*buf);
-    *buf = nullptr;
-    *cap = 0;
-    HIP_TRY(hipMalloc((void**)buf, bytes));
-    *cap = bytes;
-    return RT_OK;
-}
-
-// ---- wavefront path -------------------------------------------------------------------------
-static bool use_wavefront() {
-    const char* k = std::getenv("RT_KERNEL");
-    return k && std::strcmp(k, "wavefront") == 0;
-}
-
-static int wf_env(const char* name, int dflt, int lo, int hi) {
-    const char* v = std::getenv(name);
-    const int x = v ? std::atoi(v) : dflt;
-    return std::min(hi, std::max(lo, x));
-}
-
-static bool wf_debug() {
-    const char* v = std::getenv("RT_WF_DEBUG");
-    return v && v[0] == '1';
-}
-
-// trace-kernel waves per SIMD (register cap); RT_WF_WPE overrides for A/B runs
-static int wf_wpe() {
-    return wf_env("RT_WF_WPE", 4, 2, 4) >= 4 ? 4 : 2;  // 6 and 8 do not fit: the kernel needs ~105 VGPRs
-}
-
-template <bool COUNT, int BW>
-static void wf_launch_trace(int grid, hipStream_t st, const KParams& K, const WfBufs& W) {
-    switch (wf_wpe()) {
-        case 4: hipLaunchKernelGGL((wf_trace_kernel<COUNT, 4, BW>), dim3(grid), dim3(64), 0, st, K, W); break;
-        default: hipLaunchKernelGGL((wf_trace_kernel<COUNT, 2, BW>), dim3(grid), dim3(64), 0, st, K, W); break;
+// batches (n_views > 1) advance whole waves (C3, 8 views: refill 24 -> 64 = 1.59 -> 1.37 ms/frame)
+// with lane groups for the stragglers (16 views 1.29 -> 1.17 ms/frame); then the context's options
+static void shape_options(const rt_ctx* c, KParams& K) {
+    if (K.n_views > 1) {
+        K.refill = 64;
+        K.coop = 2;
     }
-}
-
-template <bool COUNT>
-static void wf_trace(const rt_ctx* c, int grid, hipStream_t st, KParams K, const WfBufs& W) {
-    K.S = c->S8;
-    if (c->bw == 4)
-        wf_launch_trace<COUNT, 4>(grid, st, K, W);
-    else
-        wf_launch_trace<COUNT, 8>(grid, st, K, W);
-}
-
-static int wf_trace_grid(rt_ctx* c) {
-    const int w = wf_wpe();
-    const int slot = (w == 8) ? 4 : (w == 6) ? 3 : (w == 4) ? 2 : 1;
-    if (c->wf_trace_blocks[slot] > 0) return c->wf_trace_blocks[slot];
-    int cus = 0, per_cu = 0;
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
-    hipError_t e;
-    switch (w) {
-        case 4: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wf_trace_kernel<false, 4, 8>, 64, 0); break;
-        default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wf_trace_kernel<false, 2, 8>, 64, 0); break;
-    }
-    if (e != hipSuccess || per_cu <= 0) per_cu = 4 * w;
-    c->wf_trace_blocks[slot] = std::max(1, cus) * per_cu;
-    return c->wf_trace_blocks[slot];
-}
-
-// One frame (or one rt_shade batch) as seed -> (trace -> shade)* iterations until every
-// sub-queue is empty.  The lengths live on the device; the host checks their sum every `batch`
-// iterations (kernels of an empty queue return at once).  trace_ms sums the trace launches.
-static int launch_wavefront(rt_ctx* c, const KParams& K0, const JobSrc& J, hipStream_t st, int count_mode,
-                            float* trace_ms, int* trace_launches) {
-    KParams K = K0;
-    K.S = c->S8;  // records are addressed in the wide BVH's leaf order by trace and shade alike
-    const int njobs = J.njobs;
-    if (njobs <= 0) return RT_OK;
-    if (c->bw <= 2) {
-        set_error("wavefront path needs the wide BVH (RT_BVH=4 or 8)");
-        return RT_ERR_INVALID;
-    }
-    const int nchunks = (njobs + 63) / 64;
-    const int seg = ((nchunks + WF_NQ - 1) / WF_NQ) * 64;
-    const int cap = seg * WF_NQ;
-    const int fpj = K.max_level + 1;  // frames 0..max_level (the deepest keeps its shading kd)
-    int rc = ensure(c, &c->d_wf_st, &c->wf_st_bytes, (size_t)2 * WF_NFIELDS * cap * sizeof(float));
-    if (rc != RT_OK) return rc;
-    rc = ensure(c, &c->d_wf_res, &c->wf_res_bytes, (size_t)2 * cap * sizeof(float));
-    if (rc != RT_OK) return rc;
-    rc = ensure(c, &c->d_wf_frames, &c->wf_frames_bytes, (size_t)njobs * fpj * sizeof(Frame));
-    if (rc != RT_OK) return rc;
-    const size_t cnt_ints = (size_t)WF_C_KINDS * WF_NQ * WF_CSTRIDE + 64;
-    if (!c->d_wf_cnt) HIP_TRY(hipMalloc((void**)&c->d_wf_cnt, cnt_ints * sizeof(int)));
-    if (!c->h_wf_cnt) HIP_TRY(hipHostMalloc((void**)&c->h_wf_cnt, WF_NQ * sizeof(int)));
-    int* cn[2] = {c->d_wf_cnt + (size_t)WF_C_N0 * WF_NQ * WF_CSTRIDE, c->d_wf_cnt + (size_t)WF_C_N1 * WF_NQ * WF_CSTRIDE};
-    int* chead = c->d_wf_cnt + (size_t)WF_C_HEAD * WF_NQ * WF_CSTRIDE;
-    int* crays = c->d_wf_cnt + (size_t)WF_C_RAYS * WF_NQ * WF_CSTRIDE;
-    int* ctotal = c->d_wf_cnt + (size_t)WF_C_KINDS * WF_NQ * WF_CSTRIDE;
-    int cus = 0;
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
-    // both grids are multiples of WF_NQ (block b serves sub-queue b % WF_NQ)
-    int tgrid = std::max(WF_NQ, (wf_trace_grid(c) / WF_NQ) * WF_NQ);
-    if (const char* g = std::getenv("RT_WF_TGRID")) tgrid = std::max(WF_NQ, (std::atoi(g) / WF_NQ) * WF_NQ);
-    const int sgrid = std::max(WF_NQ, (std::max(1, cus) * 8 / WF_NQ) * WF_NQ);
-    float* st0 = c->d_wf_st;
-    float* st1 = c->d_wf_st + (size_t)WF_NFIELDS * cap;
-    WfBufs W{};
-    W.cap = cap;
-    W.seg = seg;
-    W.res_t = c->d_wf_res;
-    W.res_rec = reinterpret_cast<int*>(c->d_wf_res + cap);
-    W.frames = reinterpret_cast<Frame*>(c->d_wf_frames);
-    W.fpj = fpj;
-    W.refill = wf_env("RT_WF_REFILL", 8, 1, 64);
-    W.leaf_batch = wf_env("RT_WF_LEAFBATCH", 0, 0, 64);
-    W.head = chead;
-    W.rays = crays;
-    // seed -> queue 0; sub-queue q holds the jobs of chunks q, q + WF_NQ, ...
-    HIP_TRY(hipMemsetAsync(c->d_wf_cnt, 0, cnt_ints * sizeof(int), st));
-    hipLaunchKernelGGL(wf_seed_counts_kernel, dim3(1), dim3(WF_NQ), 0, st, cn[0], njobs);
-    W.st_out = st0;
-    const int seed_grid = (int)std::min<long long>(((long long)njobs + 63) / 64, (long long)std::max(1, cus) * 16);
-    hipLaunchKernelGGL(wf_seed_kernel, dim3(seed_grid), dim3(64), 0, st, K, J, W);
-    HIP_TRY(hipGetLastError());
-    const int batch = wf_env("RT_WF_BATCH", 4, 1, 64);
-    const bool timed = (trace_ms != nullptr);
-    int cur = 0, launches = 0;
-    std::vector<std::pair<int, int>> evs;  // event indices per trace launch
-    for (int iter = 0;;) {
-        for (int b = 0; b < batch; ++b, ++iter) {
-            const int out = 1 - cur;
-            W.st_in = cur ? st1 : st0;
-            W.n_in = cn[cur];
-            W.st_out = out ? st1 : st0;
-            W.n_out = cn[out];
-            hipLaunchKernelGGL(wf_reset_kernel, dim3(1), dim3(WF_NQ), 0, st, W.n_out, W.head);
-            if (timed) {
-                const size_t need = 2 * (evs.size() + 1);
-                while (c->wf_ev.size() < need) {
-                    hipEvent_t e;
-                    HIP_TRY(hipEventCreate(&e));
-                    c->wf_ev.push_back(e);
-                }
-                const int e0 = (int)(2 * evs.size());
-                evs.push_back({e0, e0 + 1});
-                HIP_TRY(hipEventRecord(c->wf_ev[e0], st));
-            }
-            if (count_mode)
-                wf_trace<true>(c, tgrid, st, K, W);
-            else
-                wf_trace<false>(c, tgrid, st, K, W);
-            if (timed) HIP_TRY(hipEventRecord(c->wf_ev[evs.back().second], st));
-            ++launches;
-            if (count_mode)
-                hipLaunchKernelGGL(wf_shade_kernel<true>, dim3(sgrid), dim3(64), 0, st, K, J, W);
-            else
-                hipLaunchKernelGGL(wf_shade_kernel<false>, dim3(sgrid), dim3(64), 0, st, K, J, W);
-            HIP_TRY(hipGetLastError());
-            cur = out;
-            if (wf_debug()) {  // RT_WF_DEBUG=1: per-iteration queue length and trace time (synchronous)
-                hipLaunchKernelGGL(wf_total_kernel, dim3(1), dim3(WF_NQ), 0, st, W.n_in, ctotal);
-                HIP_TRY(hipMemcpyAsync(c->h_wf_cnt, ctotal, sizeof(int), hipMemcpyDeviceToHost, st));
-                HIP_TRY(hipStreamSynchronize(st));
-                float ms = 0.0f;
-                if (timed) hipEventElapsedTime(&ms, c->wf_ev[evs.back().first], c->wf_ev[evs.back().second]);
-                std::fprintf(stderr, "wf iter %d: queries %d trace %.3f ms\n", iter, c->h_wf_cnt[0], ms);
-            }
-        }
-        hipLaunchKernelGGL(wf_total_kernel, dim3(1), dim3(WF_NQ), 0, st, cn[cur], ctotal);
-        HIP_TRY(hipMemcpyAsync(c->h_wf_cnt, ctotal, sizeof(int), hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipStreamSynchronize(st));
-        if (c->h_wf_cnt[0] == 0) break;
-        if (iter > 1000000) {
-            set_error("wavefront: queue did not drain");
-            return RT_ERR_INVALID;
-        }
-    }
-    hipLaunchKernelGGL(wf_finish_kernel, dim3(1), dim3(WF_NQ), 0, st, crays, c->d_stats);
-    HIP_TRY(hipGetLastError());
-    if (timed) {
-        float tot = 0.0f;
-        for (auto& e : evs) {
-            float ms = 0.0f;
-            HIP_TRY(hipEventElapsedTime(&ms, c->wf_ev[e.first], c->wf_ev[e.second]));
-            tot += ms;
-        }
-        *trace_ms = tot;
-    }
-    if (trace_launches) *trace_launches = launches;
-    return RT_OK;
-}
-
-// primary packet pass (rt_packet.hip) ahead of the megakernels; RT_PACKET=0 disables it
-static bool use_packets(const rt_ctx* c, const KParams& K) {
-    const char* v = std::getenv("RT_PACKET");
-    if (!v || v[0] != '1') return false;  // opt-in: measured slower than the megakernels' own primaries
-    // one camera ray per pixel; the shared stack holds at most (width-1) entries per level
-    return c->bw > 2 && !K.aa && !K.multi && c->bvh8_depth * (c->bw - 1) + 2 <= PK_STACK;
-}
-
-static int launch_packets(rt_ctx* c, KParams& K, hipStream_t st, int count_mode, int njobs) {
-    int rc = ensure(c, &c->d_pre, &c->pre_bytes, (size_t)2 * njobs * sizeof(float));
-    if (rc != RT_OK) return rc;
-    K.pre_t = c->d_pre;
-    K.pre_rec = reinterpret_cast<const int*>(c->d_pre + njobs);
-    KParams Kp = K;
-    Kp.S = c->S8;
-    int cus = 0;
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
-    const int ntiles = (njobs + 63) / 64;
-    const int grid = std::min(ntiles, std::max(1, cus) * 16);
-    float* pt = c->d_pre;
-    int* pr = reinterpret_cast<int*>(c->d_pre + njobs);
-    if (c->bw == 4) {
-        if (count_mode)
-            hipLaunchKernelGGL((primary_packet_kernel<true, 4>), dim3(grid), dim3(64), 0, st, Kp, pt, pr, ntiles);
-        else
-            hipLaunchKernelGGL((primary_packet_kernel<false, 4>), dim3(grid), dim3(64), 0, st, Kp, pt, pr, ntiles);
-    } else {
-        if (count_mode)
-            hipLaunchKernelGGL((primary_packet_kernel<true, 8>), dim3(grid), dim3(64), 0, st, Kp, pt, pr, ntiles);
-        else
-            hipLaunchKernelGGL((primary_packet_kernel<false, 8>), dim3(grid), dim3(64), 0, st, Kp, pt, pr, ntiles);
-    }
-    HIP_TRY(hipGetLastError());
-    return RT_OK;
-}
-
-// Longest-first schedule: primary pass + hit-first job order (rt_schedule.hip).  RT_SCHED=0
-// disables it; it needs one camera ray per pixel and the wide BVH.
-static bool use_schedule(const rt_ctx* c, const KParams& K) {
-    const char* v = std::getenv("RT_SCHED");
-    if (!v || v[0] != '1') return false;  // opt-in: measured no gain
-    return c->bw > 2 && !K.aa && !K.multi;
-}
-
-static int launch_schedule(rt_ctx* c, KParams& K, hipStream_t st, int count_mode, int njobs) {
-    const int ntiles = (njobs + 63) / 64;
-    int rc = ensure(c, &c->d_pre, &c->pre_bytes, (size_t)2 * njobs * sizeof(float));
-    if (rc != RT_OK) return rc;
-    rc = ensure(c, &c->d_sched, &c->sched_bytes, ((size_t)2 * (ntiles + 1) + njobs) * sizeof(int));
-    if (rc != RT_OK) return rc;
-    float* pt = c->d_pre;
-    int* pr = reinterpret_cast<int*>(c->d_pre + njobs);
-    int* hits = reinterpret_cast<int*>(c->d_sched);
-    int* off = hits + (ntiles + 1);
-    int* order = off + (ntiles + 1);
-    KParams Kp = K;
-    Kp.S = c->S8;
-    int cus = 0;
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
-    const int grid = std::min(ntiles, std::max(1, cus) * 16);
-    if (c->bw == 4) {
-        if (count_mode)
-            hipLaunchKernelGGL((primary_kernel<true, 4>), dim3(grid), dim3(64), 0, st, Kp, pt, pr, hits, ntiles);
-        else
-            hipLaunchKernelGGL((primary_kernel<false, 4>), dim3(grid), dim3(64), 0, st, Kp, pt, pr, hits, ntiles);
-    } else {
-        if (count_mode)
-            hipLaunchKernelGGL((primary_kernel<true, 8>), dim3(grid), dim3(64), 0, st, Kp, pt, pr, hits, ntiles);
-        else
-            hipLaunchKernelGGL((primary_kernel<false, 8>), dim3(grid), dim3(64), 0, st, Kp, pt, pr, hits, ntiles);
-    }
-    hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, st, hits, off, ntiles);
-    hipLaunchKernelGGL(job_order_kernel, dim3(grid), dim3(64), 0, st, pr, off, order, Kp, ntiles);
-    HIP_TRY(hipGetLastError());
-    K.pre_t = pt;
-    K.pre_rec = pr;
-    K.job_order = order;
-    return RT_OK;
-}
-
-// RT_SCHED=2: jobs ordered by the previous frame's per-pixel query counts (most expensive first).
-static int launch_cost_schedule(rt_ctx* c, KParams& K, hipStream_t st, int njobs) {
-    const int nblk = (njobs + CS_BLOCK - 1) / CS_BLOCK;
-    const size_t bytes = ((size_t)2 * njobs + (size_t)CS_BUCKETS * nblk) * sizeof(int);
-    const long long key = ((long long)K.W * 65536 + K.H) * 4096 + (long long)K.band_rank * 64 + K.band_count +
-                          ((long long)K.band_rows << 40);
-    const bool fresh = (c->cost_bytes < bytes) || (c->cost_key != key);
-    int rc = ensure(c, &c->d_cost, &c->cost_bytes, bytes);
-    if (rc != RT_OK) return rc;
-    int* cost = reinterpret_cast<int*>(c->d_cost);
-    int* hist = cost + njobs;
-    int* order = hist + (size_t)CS_BUCKETS * nblk;
-    if (fresh) {
-        HIP_TRY(hipMemsetAsync(cost, 0, (size_t)njobs * sizeof(int), st));
-        c->cost_key = key;
-    } else {
-        hipLaunchKernelGGL(cost_hist_kernel, dim3(nblk), dim3(CS_BLOCK), 0, st, cost, njobs, hist);
-        hipLaunchKernelGGL(cost_scan_kernel, dim3(1), dim3(1024), 0, st, hist, CS_BUCKETS * nblk);
-        hipLaunchKernelGGL(cost_scatter_kernel, dim3(nblk), dim3(CS_BLOCK), 0, st, cost, njobs, hist, order);
-        HIP_TRY(hipGetLastError());
-        K.job_order = order;
-    }
-    K.job_cost = cost;
-    return RT_OK;
+    if (c->opt_refill > 0) K.refill = c->opt_refill;
+    if (c->opt_coop >= 0) K.coop = c->opt_coop;
+    if (c->opt_coop_max > 0) K.coop_max = std::min(K.coop_max, c->opt_coop_max);
+    if (K.coop_max <= 0) K.coop = 0;
 }
 
 static int launch_render(rt_ctx* c, KParams& K, hipStream_t st, int count_mode, rt_stats* stats) {
     const int tiles_x = (K.W + 7) / 8;
     const int tiles_y = (K.band_rows + 7) / 8;
     const long long blocks = (long long)tiles_x * tiles_y * K.n_local_bands;
-    float trace_ms = 0.0f;
-    int trace_launches = 0;
+    shape_options(c, K);
     HIP_TRY(hipMemsetAsync(c->d_stats, 0, RT_STATS_BYTES, st));
     if (blocks > 0) {
-        HIP_TRY(hipEventRecord(c->ev0, st));
-        if (use_wavefront() && c->bw > 2) {
-            JobSrc J{};
-            J.mode = 0;
-            J.njobs = (int)(blocks * 64);
-            J.n_views = 1;
-            J.view_jobs = J.njobs;
-            int rc = launch_wavefront(c, K, J, st, count_mode, stats ? &trace_ms : nullptr,
-                                      stats ? &trace_launches : nullptr);
+        JobSrc J{};
+        J.mode = 0;
+        J.n_views = std::max(1, K.n_views);
+        J.view_jobs = (int)(blocks * 64);
+        J.njobs = J.n_views * J.view_jobs;
+        K.view_jobs = J.view_jobs;
+        J.counter = reinterpret_cast<int*>(c->d_stats + 7);
+        J.xq = use_df(c) ? reinterpret_cast<int*>(c->d_stats + 16) : nullptr;
+        const int grid = (int)std::min<long long>(blocks * J.n_views, persistent_grid(c));
+        if (c->opt_wave_trace) {
+            const int rc = ensure(c, &c->d_wave_trace, &c->wave_trace_bytes, (size_t)grid * 8 * 8);
             if (rc != RT_OK) return rc;
-        } else if (use_tile_kernel()) {
-            if (count_mode)
-                hipLaunchKernelGGL(render_kernel<true>, dim3((unsigned)blocks), dim3(64), 0, st, K);
-            else
-                hipLaunchKernelGGL(render_kernel<false>, dim3((unsigned)blocks), dim3(64), 0, st, K);
-        } else {
-            JobSrc J{};
-            J.mode = 0;
-            J.n_views = std::max(1, K.n_views);
-            J.view_jobs = (int)(blocks * 64);
-            J.njobs = J.n_views * J.view_jobs;
-            K.view_jobs = J.view_jobs;
-            J.counter = reinterpret_cast<int*>(c->d_stats + 7);
-            J.xq = use_xcd_queues() ? reinterpret_cast<int*>(c->d_stats + 16) : nullptr;
-            if (use_packets(c, K)) {
-                const int rc = launch_packets(c, K, st, count_mode, J.njobs);
-                if (rc != RT_OK) return rc;
-            } else if (use_schedule(c, K)) {
-                const int rc = launch_schedule(c, K, st, count_mode, J.njobs);
-                if (rc != RT_OK) return rc;
-            }
-            const char* cs = std::getenv("RT_SCHED");
-            if (cs && cs[0] == '2' && !K.job_order) {
-                const int rc = launch_cost_schedule(c, K, st, J.njobs);
-                if (rc != RT_OK) return rc;
-            }
-            const int grid = (int)std::min<long long>(blocks, persistent_grid(c));
-            const char* wt = std::getenv("RT_WAVE_TRACE");
-            if (wt && wt[0] == '1') {
-                const int rc = ensure(c, &c->d_wave_trace, &c->wave_trace_bytes, (size_t)grid * 8 * 8);
-                if (rc != RT_OK) return rc;
-                K.wave_trace = reinterpret_cast<unsigned long long*>(c->d_wave_trace);
-                c->wave_trace_n = grid;
-            }
-            if (count_mode)
-                launch_persistent<true>(grid, st, K, J, c);
-            else
-                launch_persistent<false>(grid, st, K, J, c);
+            K.wave_trace = reinterpret_cast<unsigned long long*>(c->d_wave_trace);
+            c->wave_trace_n = grid;
         }
+        HIP_TRY(hipEventRecord(c->ev0, st));
+        const int lrc = count_mode ? launch_persistent<true>(grid, st, K, J, c) : launch_persistent<false>(grid, st, K, J, c);
+        if (lrc != RT_OK) return lrc;
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(c->ev1, st));
     }
     if (stats) {
-        unsigned long long h[8] = {0};
+        unsigned long long h[13] = {0};
         HIP_TRY(hipMemcpyAsync(h, c->d_stats, sizeof(h), hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
+        std::memset(stats, 0, sizeof(*stats));
         stats->rays = h[0];
         stats->node_visits = h[1];
         stats->tri_tests = h[2];
         stats->hits = h[3];
+        stats->ub_hits = h[12];
         float ms = 0.0f;
         if (blocks > 0) HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
         stats->kernel_ms = ms;
-        stats->node_bytes = (use_tile_kernel() || c->bw == 2) ? 64u : 128u;
-        stats->trace_ms = trace_ms;
-        stats->trace_launches = (uint32_t)trace_launches;
+        stats->node_bytes = 128u;  // quantised BVH8 node
+        std::memcpy(stats->kernel, c->last_kernel, sizeof(stats->kernel));
+        stats->kernel[sizeof(stats->kernel) - 1] = 0;
     }
     return RT_OK;
 }
@@ -1066,16 +816,8 @@ extern "C" int rt_render_device(rt_ctx* c, const rt_camera* cam, const rt_params
     K.band_rank = band_rank;
     K.band_count = band_count;
     K.n_local_bands = nbands > band_rank ? (nbands - band_rank + band_count - 1) / band_count : 0;
+    K.view_rows = K.n_local_bands * band_rows;
     K.out = d_out;
-    // Few shadow samples per shading point (point/spot lights: long mirror and camera queries):
-    // full-wave refill + lane groups for the stragglers (C3 2.37 -> 2.18 ms).  Sample-heavy
-    // lights (sphere/plane lights, many short shadow queries) keep the 24-lane refill (C4 43.6 ms
-    // against 48.5 ms with it).
-    if (!std::getenv("RT_REFILL") && !std::getenv("RT_COOP") && K.coop == 1 &&
-        K.S.nsl * K.sl_count + K.S.nplane * K.plane_k * K.plane_k <= 4) {
-        K.refill = 64;
-        K.coop = 2;
-    }
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     return launch_render(c, K, st, g_count_mode, stats);
 }
@@ -1090,10 +832,6 @@ extern "C" int rt_render_views_device(rt_ctx* c, const rt_camera* cams, int n_vi
     }
     if (n_views == 1)
         return rt_render_device(c, cams, p, W, H, band_rows, band_rank, band_count, d_out, stream, stats);
-    if (use_wavefront() || use_tile_kernel() || (std::getenv("RT_PACKET") && std::getenv("RT_PACKET")[0] == '1') || std::getenv("RT_SCHED")) {
-        set_error("rt_render_views_device: view batches run on the persistent kernels only");
-        return RT_ERR_INVALID;
-    }
     HIP_TRY(hipSetDevice(c->device));
     KParams K;
     int rc = fill_params(c, cams, p, W, H, K);
@@ -1109,12 +847,6 @@ extern "C" int rt_render_views_device(rt_ctx* c, const rt_camera* cams, int n_vi
         return RT_ERR_INVALID;
     }
     K.out = d_out;
-    // dynamic-fetch refill threshold: in a batch only the last frame drains, and advancing all 64
-    // lanes at once amortises the state machine's spills best (C3, 8 views: 24 -> 64 lanes = 1.59 ->
-    // 1.37 ms/frame); the last queries a full-wave refill waits for go to lane groups (coop 2:
-    // C3, 16 views, 1.29 -> 1.17 ms/frame; C4 neutral)
-    if (!std::getenv("RT_REFILL")) K.refill = 64;
-    if (!std::getenv("RT_COOP") && K.coop == 1) K.coop = 2;
     K.n_views = n_views;
     K.view_rows = K.n_local_bands * band_rows;
     std::vector<float> v((size_t)n_views * 12, 0.0f);
@@ -1144,6 +876,21 @@ extern "C" int rt_unpermute_bands_device(int W, int H, int band_rows, int band_c
     const size_t total = (size_t)W * H;
     hipLaunchKernelGGL(unpermute_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, W,
                        H, band_rows, band_count, max_local, d_gathered, d_image);
+    HIP_TRY(hipGetLastError());
+    return RT_OK;
+}
+
+extern "C" int rt_unpermute_views_device(int W, int H, int band_rows, int band_count, int n_views,
+                                         const float* d_gathered, float* d_images, void* stream) {
+    if (W <= 0 || H <= 0 || band_rows <= 0 || band_count <= 0 || n_views <= 0 || !d_gathered || !d_images) {
+        set_error("rt_unpermute_views_device: invalid argument");
+        return RT_ERR_INVALID;
+    }
+    const int nbands = (H + band_rows - 1) / band_rows;
+    const int max_local = (nbands + band_count - 1) / band_count;
+    const size_t total = (size_t)W * H * n_views;
+    hipLaunchKernelGGL(unpermute_views_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       W, H, band_rows, band_count, max_local, n_views, d_gathered, d_images);
     HIP_TRY(hipGetLastError());
     return RT_OK;
 }
@@ -1216,12 +963,12 @@ extern "C" int rt_intersect(rt_ctx* c, const rt_ray* rays, int n, int use_bvh, r
         set_error("rt_intersect: hipMalloc failed");
         return RT_ERR_HIP;
     }
-    KParams K;
-    std::memset(&K, 0, sizeof(K));
-    K.S = c->S;
-    hipMemcpy(d_r, rays, sizeof(rt_ray) * n, hipMemcpyHostToDevice);
-    hipLaunchKernelGGL(intersect_kernel, dim3((n + 63) / 64), dim3(64), 0, c->stream, K, d_r, n, use_bvh ? 1 : 0, d_h);
-    hipError_t e = hipGetLastError();
+    hipError_t e = hipMemcpy(d_r, rays, sizeof(rt_ray) * n, hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(intersect_kernel, dim3((n + 63) / 64), dim3(64), 0, c->stream, c->S, d_r, n, use_bvh ? 1 : 0,
+                           d_h);
+        e = hipGetLastError();
+    }
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e == hipSuccess) e = hipMemcpy(hits, d_h, sizeof(rt_hit) * n, hipMemcpyDeviceToHost);
     hipFree(d_r);
@@ -1243,33 +990,16 @@ extern "C" int rt_shade(rt_ctx* c, const rt_ray* rays, int n, const rt_params* p
     KParams K;
     int rc = fill_params(c, nullptr, p, 1, 1, K);
     if (rc != RT_OK) return rc;
+    shape_options(c, K);
     rt_ray* d_r = nullptr;
     float* d_c = nullptr;
     unsigned long long* d_n = nullptr;
-    HIP_TRY(hipMalloc(&d_r, sizeof(rt_ray) * n));
-    HIP_TRY(hipMalloc(&d_c, sizeof(float) * 3 * n));
-    HIP_TRY(hipMalloc(&d_n, sizeof(unsigned long long) * n));
-    hipMemcpy(d_r, rays, sizeof(rt_ray) * n, hipMemcpyHostToDevice);
-    if (use_wavefront() && c->bw > 2) {
-        JobSrc J{};
-        J.mode = 1;
-        J.njobs = n;
-        J.n_views = 1;
-        J.view_jobs = n;
-        J.rays = d_r;
-        J.rgb = d_c;
-        J.ray_counts = d_n;
-        hipMemsetAsync(c->d_stats, 0, RT_STATS_BYTES, c->stream);
-        const int rc = launch_wavefront(c, K, J, c->stream, 0, nullptr, nullptr);
-        if (rc != RT_OK) {
-            hipFree(d_r);
-            hipFree(d_c);
-            hipFree(d_n);
-            return rc;
-        }
-    } else if (use_tile_kernel()) {
-        hipLaunchKernelGGL(shade_kernel, dim3((n + 63) / 64), dim3(64), 0, c->stream, K, d_r, n, d_c, d_n);
-    } else {
+    hipError_t e = hipMalloc(&d_r, sizeof(rt_ray) * n);
+    if (e == hipSuccess) e = hipMalloc(&d_c, sizeof(float) * 3 * n);
+    if (e == hipSuccess) e = hipMalloc(&d_n, sizeof(unsigned long long) * n);
+    if (e == hipSuccess) e = hipMemcpy(d_r, rays, sizeof(rt_ray) * n, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemsetAsync(c->d_stats, 0, RT_STATS_BYTES, c->stream);
+    if (e == hipSuccess) {
         JobSrc J{};
         J.mode = 1;
         J.njobs = n;
@@ -1279,18 +1009,17 @@ extern "C" int rt_shade(rt_ctx* c, const rt_ray* rays, int n, const rt_params* p
         J.n_views = 1;
         J.view_jobs = n;
         J.counter = reinterpret_cast<int*>(c->d_stats + 7);
-        J.xq = use_xcd_queues() ? reinterpret_cast<int*>(c->d_stats + 16) : nullptr;
-        hipMemsetAsync(c->d_stats, 0, RT_STATS_BYTES, c->stream);
+        J.xq = use_df(c) ? reinterpret_cast<int*>(c->d_stats + 16) : nullptr;
         const int grid = std::min((n + 63) / 64, persistent_grid(c));
-        launch_persistent<false>(grid, c->stream, K, J, c);
+        if (launch_persistent<false>(grid, c->stream, K, J, c) != RT_OK) e = hipErrorInvalidValue;
+        else e = hipGetLastError();
     }
-    hipError_t e = hipGetLastError();
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e == hipSuccess) e = hipMemcpy(rgb, d_c, sizeof(float) * 3 * n, hipMemcpyDeviceToHost);
     if (e == hipSuccess && ray_counts) e = hipMemcpy(ray_counts, d_n, sizeof(uint64_t) * n, hipMemcpyDeviceToHost);
-    hipFree(d_r);
-    hipFree(d_c);
-    hipFree(d_n);
+    if (d_r) hipFree(d_r);
+    if (d_c) hipFree(d_c);
+    if (d_n) hipFree(d_n);
     if (e != hipSuccess) {
         set_error(std::string("rt_shade: ") + hipGetErrorString(e));
         return RT_ERR_HIP;
@@ -1298,8 +1027,39 @@ extern "C" int rt_shade(rt_ctx* c, const rt_ray* rays, int n, const rt_params* p
     return RT_OK;
 }
 
-// Debug counters of the last counting launch: [8..13] per-query node-visit histogram
-// (<16, <64, <256, <1024, <4096, >=4096), [14] max node visits, [15] max triangle records.
+// Image::getPixel(uv, lod) of texture `texture` under the params' filtering / out-of-bounds rules
+// for n (u, v, lod) triples (host buffers): the device sampler the renderer calls, for parity tests.
+extern "C" int rt_texture_sample(rt_ctx* c, int texture, int n, const float* uv_lod, const rt_params* p, float* rgb) {
+    if (!c || !p || n < 0 || (n > 0 && (!uv_lod || !rgb)) || texture < 0 || texture >= c->S.ntex) {
+        set_error("rt_texture_sample: invalid argument");
+        return RT_ERR_INVALID;
+    }
+    if (n == 0) return RT_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    KParams K;
+    int rc = fill_params(c, nullptr, p, 1, 1, K);
+    if (rc != RT_OK) return rc;
+    float *d_in = nullptr, *d_out = nullptr;
+    hipError_t e = hipMalloc(&d_in, sizeof(float) * 3 * n);
+    if (e == hipSuccess) e = hipMalloc(&d_out, sizeof(float) * 3 * n);
+    if (e == hipSuccess) e = hipMemcpy(d_in, uv_lod, sizeof(float) * 3 * n, hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(tex_sample_kernel, dim3((n + 255) / 256), dim3(256), 0, c->stream, K.S, texture, d_in, n,
+                           d_out);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess) e = hipMemcpy(rgb, d_out, sizeof(float) * 3 * n, hipMemcpyDeviceToHost);
+    if (d_in) hipFree(d_in);
+    if (d_out) hipFree(d_out);
+    if (e != hipSuccess) {
+        set_error(std::string("rt_texture_sample: ") + hipGetErrorString(e));
+        return RT_ERR_HIP;
+    }
+    return RT_OK;
+}
+
+// Developer counters of the last counting launch ([8..11] state-machine / traversal clocks).
 extern "C" int rt_debug_counters(rt_ctx* c, uint64_t* out, int n) {
     if (!c || !out || n <= 0) return RT_ERR_INVALID;
     unsigned long long h[16] = {0};

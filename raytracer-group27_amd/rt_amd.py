@@ -99,8 +99,13 @@ class rt_hit(C.Structure):
 
 class rt_stats(C.Structure):
     _fields_ = [("rays", C.c_uint64), ("node_visits", C.c_uint64), ("tri_tests", C.c_uint64),
-                ("hits", C.c_uint64), ("kernel_ms", C.c_float), ("node_bytes", C.c_uint32),
-                ("trace_ms", C.c_float), ("trace_launches", C.c_uint32)]
+                ("hits", C.c_uint64), ("ub_hits", C.c_uint64), ("kernel_ms", C.c_float), ("node_bytes", C.c_uint32),
+                ("kernel", C.c_char * 64)]
+
+    @property
+    def kernel_name(self):
+        """The launched render kernel as rocprofv3 names it (without the argument list)."""
+        return self.kernel.decode()
 
 
 RAY_DTYPE = np.dtype([("origin", "<f4", 3), ("direction", "<f4", 3), ("t", "<f4")])
@@ -117,8 +122,17 @@ EXPORTS = [
     "rt_destroy", "rt_render", "rt_render_device", "rt_render_views_device", "rt_render_views", "rt_unpermute_bands_device", "rt_intersect", "rt_shade",
     "rt_set_counting", "rt_debug_counters", "rt_ctx_info", "rt_selftest_math",
     "rt_postprocess_device", "rt_bitmap_device", "rt_postprocess", "rt_bitmap", "rt_encode_bmp", "rt_write_bmp",
-    "rt_philox4x32_10", "rt_debug_wave_trace", "rt_decode_png",
+    "rt_philox4x32_10", "rt_debug_wave_trace", "rt_decode_png", "rt_ctx_set_option", "rt_texture_sample",
+    "rt_update_lights", "rt_update_materials", "rt_unpermute_views_device",
 ]
+
+# rt_ctx_set_option (include/rt_amd.h): test / developer hooks; defaults are the shipped path
+OPT_KERNEL, OPT_COOP, OPT_COOP_MAX, OPT_REFILL, OPT_WAVE_TRACE, OPT_VARIANT = 1, 2, 3, 4, 5, 6
+KERNEL_AUTO, KERNEL_WHOLE_TRAVERSAL, KERNEL_DYNAMIC_FETCH = 0, 1, 2
+# compiled kernel variants (rt_megakernel.hip RT_V_*, rt_runtime.hip kDfVariants / kWtVariants)
+V_CALL, V_NOPF, V_NOCOOP, V_W3 = 1, 2, 4, 8
+DF_VARIANTS = [V_CALL | V_NOPF, 0, V_CALL, V_CALL | V_NOPF | V_NOCOOP | V_W3]
+WT_VARIANTS = [V_CALL | V_W3, 0]
 
 class rt_post_params(C.Structure):
     """Screen post-processing settings (src/screen.h:58-111), raw setter values."""
@@ -221,6 +235,7 @@ def lib():
             "rt_render_views": ([vp, P(rt_camera), C.c_int, P(rt_params), C.c_int, C.c_int, P(C.c_float),
                                  P(rt_stats)], C.c_int),
             "rt_unpermute_bands_device": ([C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp], C.c_int),
+            "rt_unpermute_views_device": ([C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp], C.c_int),
             "rt_intersect": ([vp, vp, C.c_int, C.c_int, vp], C.c_int),
             "rt_shade": ([vp, vp, C.c_int, P(rt_params), P(C.c_float), P(C.c_uint64)], C.c_int),
             "rt_set_counting": ([C.c_int], C.c_int),
@@ -237,6 +252,10 @@ def lib():
             "rt_decode_png": ([P(C.c_uint8), C.c_long, P(C.c_int), P(C.c_int), P(C.c_int), P(C.c_uint8), C.c_long],
                               C.c_int),
             "rt_debug_wave_trace": ([vp, P(C.c_uint64), C.c_int], C.c_int),
+            "rt_ctx_set_option": ([vp, C.c_int, C.c_int], C.c_int),
+            "rt_texture_sample": ([vp, C.c_int, C.c_int, P(C.c_float), P(rt_params), P(C.c_float)], C.c_int),
+            "rt_update_lights": ([vp, P(rt_scene_desc)], C.c_int),
+            "rt_update_materials": ([vp, C.c_int, P(rt_material), C.c_int, P(rt_material)], C.c_int),
         }
         for name, (args, res) in sigs.items():
             f = getattr(L, name)
@@ -470,6 +489,30 @@ class Context:
                              cnt.ctypes.data_as(C.POINTER(C.c_uint64))), "rt_shade")
         return rgb.reshape(-1, 3), cnt
 
+    def set_option(self, option, value):
+        """rt_ctx_set_option: test / developer hook (every value renders the same image)."""
+        check(lib().rt_ctx_set_option(self.h, int(option), int(value)), "rt_ctx_set_option")
+
+    def texture_sample(self, texture, uv_lod, prm):
+        """Image::getPixel(uv, lod) on the device for rows (u, v, lod); returns [n, 3] float32."""
+        a = np.ascontiguousarray(uv_lod, np.float32).reshape(-1, 3)
+        out = np.zeros((len(a), 3), np.float32)
+        check(lib().rt_texture_sample(self.h, int(texture), len(a), a.ctypes.data_as(C.POINTER(C.c_float)),
+                                      C.byref(prm), out.ctypes.data_as(C.POINTER(C.c_float))), "rt_texture_sample")
+        return out
+
+    def update_lights(self, scene):
+        """rt_update_lights: take the scene's current light arrays (ImGui light edits)."""
+        d = scene.desc()
+        check(lib().rt_update_lights(self.h, C.byref(d)), "rt_update_lights")
+
+    def update_materials(self, mesh_materials, sphere_materials=()):
+        """rt_update_materials: replace every mesh and sphere material (counts must match)."""
+        mm = (rt_material * max(1, len(mesh_materials)))(*mesh_materials)
+        sm = (rt_material * max(1, len(sphere_materials)))(*sphere_materials)
+        check(lib().rt_update_materials(self.h, len(mesh_materials), mm, len(sphere_materials), sm),
+              "rt_update_materials")
+
     def debug_counters(self):
         out = np.zeros(16, np.uint64)
         check(lib().rt_debug_counters(self.h, out.ctypes.data_as(C.POINTER(C.c_uint64)), 16))
@@ -505,6 +548,15 @@ def local_band_elems(W, H, band_rows, count):
     """Floats in one rank's (padded) band buffer: max_local_bands * band_rows * W * 3."""
     nbands = (H + band_rows - 1) // band_rows
     return ((nbands + count - 1) // count) * band_rows * W * 3
+
+
+def unpermute_views_host(gathered, W, H, band_rows, count, n_views):
+    """Host statement of unpermute_views_kernel: [count][n_views][max_local][band_rows][W][3] ->
+    n_views images in Screen::m_textureData order."""
+    nbands = (H + band_rows - 1) // band_rows
+    max_local = (nbands + count - 1) // count
+    g = np.asarray(gathered, np.float32).reshape(count, n_views, max_local * band_rows * W * 3)
+    return np.stack([unpermute_host(g[:, v].reshape(-1), W, H, band_rows, count) for v in range(n_views)])
 
 
 def unpermute_host(gathered, W, H, band_rows, count):

@@ -31,12 +31,22 @@ def test_library_exports_every_symbol(R):
 
 
 def test_abi_version_and_struct_sizes(R):
-    assert R.lib().rt_abi_version() == 3
+    assert R.lib().rt_abi_version() == 4
+    assert ctypes.sizeof(R.rt_stats) == 112
     assert ctypes.sizeof(R.rt_material) == 40
     assert ctypes.sizeof(R.rt_ray) == 28
     assert ctypes.sizeof(R.rt_hit) == 52
     assert ctypes.sizeof(R.rt_params) == 80
     assert ctypes.sizeof(R.rt_texture) == 24
+
+
+def test_library_reads_no_environment(R):
+    """Render paths are chosen by the scene and explicit context options (rt_ctx_set_option), never
+    by environment variables: the library imports no getenv / secure_getenv."""
+    import subprocess
+
+    nm = subprocess.run(["nm", "-D", "--undefined-only", R.LIB_PATH], capture_output=True, text=True, check=True)
+    assert not re.search(r"\b(secure_)?getenv\b", nm.stdout)
 
 
 def test_no_cpu_fallback_without_gpu(R):

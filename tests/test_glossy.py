@@ -58,29 +58,22 @@ def test_oracle_glossy_is_seeded(R, O):
 @pytest.mark.gpu
 @pytest.mark.parametrize("glossy,seed", [(10, 0x5EED), (4, 7), (2, 0)])
 def test_gpu_glossy_matches_oracle(R, O, glossy, seed):
-    import os
+    import variants as V
 
     s, p = _cornell(R, glossy, seed)
     W, H = 48, 27
     ctx = R.Context(s)
     cam = R.camera_from_trackball(aspect=R.aspect_of(W, H))
     ref, rays = O.Oracle(s).render(p, W, H)
-    saved = os.environ.get("RT_KERNEL")
-    try:
-        base = None
-        for k in ("persistent", "df", "wavefront"):
-            os.environ["RT_KERNEL"] = k
+    base = None
+    for v in V.all_variants(R):
+        with V.options(R, ctx, v):
             img, st = ctx.render(cam, p, W, H)
-            assert st.rays == rays, k
-            assert float(np.max(np.abs(img - ref))) <= 1e-5, k
-            if base is None:
-                base = img
-            assert img.tobytes() == base.tobytes(), k
-    finally:
-        if saved is None:
-            os.environ.pop("RT_KERNEL", None)
-        else:
-            os.environ["RT_KERNEL"] = saved
+        assert st.rays == rays, v
+        assert float(np.max(np.abs(img - ref))) <= 1e-5, v
+        if base is None:
+            base = img
+        assert img.tobytes() == base.tobytes(), v
     ctx.close()
 
 

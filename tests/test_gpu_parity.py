@@ -8,6 +8,7 @@ import os
 import numpy as np
 import pytest
 
+import variants as V
 from golden_cases import IMAGES, PRESET_IMAGES, apply
 
 pytestmark = pytest.mark.gpu
@@ -102,24 +103,53 @@ def test_full_frame_c1_c2(R, O, ctxs):
         assert float(np.max(np.abs(img - ref))) <= TOL, cfg
 
 
+def _oracle_threads():
+    """Host threads for the oracle: the box's CPU share (OMP_NUM_THREADS), not os.cpu_count()."""
+    n = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(os.cpu_count() or 1, n if n > 0 else 16))
+
+
 @pytest.mark.parametrize("cfg", ["C3", "C4", "C5"])
 def test_full_size_sampled_pixels(R, O, ctxs, cfg):
-    """Full BASELINE resolution on the GPU; a fixed pixel sample (half of them on geometry)
-    re-rendered by the oracle."""
+    """Full BASELINE resolution on the GPU; BASELINE.md's CPU sample (4 096 pixels, the first 4 096
+    of a seed-12345 permutation of the frame) re-rendered by the oracle, plus 64 pixels on
+    geometry, every one within 1e-5."""
     scene, ctx, prm, W, H = ctxs(cfg)
     img, st = ctx.render(R.camera_from_trackball(aspect=R.aspect_of(W, H)), prm, W, H)
     assert np.isfinite(img).all()
     view = img.reshape(H, W, 3)[::-1]  # [y][x] in reference y order
-    rng = np.random.default_rng(12345)
+    sel = np.random.default_rng(12345).permutation(W * H)[:4096]
     lit = np.argwhere(view.max(axis=2) > 0)
-    n = 24 if cfg != "C5" else 12
-    pick = lit[rng.choice(len(lit), size=min(n, len(lit)), replace=False)]
-    rand = np.stack([rng.integers(0, H, n), rng.integers(0, W, n)], axis=1)
-    yx = np.concatenate([pick, rand])
-    xy = yx[:, ::-1].astype(np.int32)
+    pick = lit[np.random.default_rng(7).choice(len(lit), size=min(64, len(lit)), replace=False)]
+    xy = np.concatenate([np.stack([sel % W, sel // W], axis=1), pick[:, ::-1]]).astype(np.int32)
+    O.set_threads(_oracle_threads())
     ref, _ = O.Oracle(scene).render_pixels(prm, W, H, xy)
-    got = view[yx[:, 0], yx[:, 1]]
+    got = view[xy[:, 1], xy[:, 0]]
     assert float(np.max(np.abs(got - ref))) <= TOL
+
+
+@pytest.mark.parametrize("cfg,uv,W,H", [("C2", None, 64, 48), ("C3", (200, 80), 96, 54), ("C4", (200, 80), 64, 36),
+                                        ("C5", None, 64, 36)])
+def test_ub_regime_count_matches_oracle(R, O, ctxs, cfg, uv, W, H):
+    """The counting build's ub_hits (shaded triangle hits where the reference's
+    barycentricCoordinates returns false and it interpolates uninitialised coordinates,
+    src/ray_tracing.cpp:147-157, 281-295) equals the oracle's count over the whole frame."""
+    scene, ctx, prm, _, _ = ctxs(cfg, uv)
+    cam = R.camera_from_trackball(aspect=R.aspect_of(W, H))
+    R.set_counting(True)
+    try:
+        img, st = ctx.render(cam, prm, W, H)
+    finally:
+        R.set_counting(False)
+    xs, ys = np.meshgrid(np.arange(W), np.arange(H))
+    xy = np.stack([xs.ravel(), ys.ravel()], axis=1).astype(np.int32)
+    O.set_threads(_oracle_threads())
+    _, rays, ub = O.Oracle(scene).render_pixels(prm, W, H, xy, with_ub=True)
+    assert st.rays == int(rays.sum())
+    assert st.ub_hits == int(ub.sum())
+    assert st.ub_hits <= st.hits
+    if cfg in ("C3", "C4"):
+        assert st.ub_hits > 0  # the tessellated proxy's small triangles fall below the 1e-4 area check
 
 
 @pytest.mark.parametrize("cfg,uv", [("C3", (200, 80)), ("C5", None)])
@@ -155,6 +185,36 @@ def test_band_split_bit_identical(R, ctxs, cfg, uv):
         assert rays == st.rays
 
 
+@pytest.mark.parametrize("cfg,uv", [("C3", (200, 80)), ("C2", None)])
+def test_band_split_view_batch_bit_identical(R, ctxs, cfg, uv):
+    """bench.py's N>1 step on one GPU: each rank's bands of every view in one launch, the buffers
+    back to back as all_gather_into_tensor leaves them, one rt_unpermute_views_device launch --
+    every view bit-identical to rt_render_views, ray counts add up."""
+    import ctypes
+
+    import torch
+
+    scene, ctx, prm, _, _ = ctxs(cfg, uv)
+    W, H, F = 120, 67, 3
+    cams = R.turntable_cameras(F, R.aspect_of(W, H))
+    ref, rst = ctx.render_views(cams, prm, W, H)
+    for count in (2, 3):
+        n = F * R.local_band_elems(W, H, 8, count)
+        gathered = torch.full((count * n,), -1.0, dtype=torch.float32, device="cuda")
+        rays = 0
+        for rank in range(count):
+            part = gathered[rank * n:(rank + 1) * n]
+            rays += ctx.render_views_device(cams, prm, W, H, 8, rank, count, part.data_ptr(), None).rays
+        imgs = torch.zeros(F * W * H * 3, dtype=torch.float32, device="cuda")
+        R.check(R.lib().rt_unpermute_views_device(W, H, 8, count, F, ctypes.c_void_p(gathered.data_ptr()),
+                                                  ctypes.c_void_p(imgs.data_ptr()), None))
+        torch.cuda.synchronize()
+        got = imgs.cpu().numpy().reshape(F, -1)
+        assert got.tobytes() == ref.tobytes(), count
+        assert R.unpermute_views_host(gathered.cpu().numpy(), W, H, 8, count, F).tobytes() == ref.tobytes()
+        assert rays == rst.rays
+
+
 def test_device_math_is_ieee(R, ctxs):
     _, ctx, _, _, _ = ctxs("C1")
     rng = np.random.default_rng(3)
@@ -181,63 +241,44 @@ def test_invalid_params_fail_loudly(R, ctxs):
         ctx.render(R.camera_from_trackball(), bad, 8, 8)
 
 
-KERNEL_VARIANTS = [
-    {"RT_KERNEL": "persistent"},
-    {"RT_KERNEL": "df"},
-    {"RT_KERNEL": "df", "RT_LEAFBATCH": "64"},
-    {"RT_KERNEL": "df", "RT_COOP": "0"},          # no cooperative drain traversal
-    {"RT_KERNEL": "df", "RT_COOP_MAX": "1"},      # drain groups of 64 lanes only
-    {"RT_KERNEL": "df", "RT_SCHED": "2"},         # cost-ordered job hand-out
-    {"RT_KERNEL": "wavefront"},
-    {"RT_KERNEL": "tile"},
-    {"RT_KERNEL": "persistent", "RT_PACKET": "1"},
-    {"RT_KERNEL": "df", "RT_PACKET": "1"},
-]
-
-
 @pytest.mark.parametrize("case", ["c2_64x48", "c3s_96x54", "c4s_64x36", "c5_96x54", "c5_depth3_bvh_64x36"])
 def test_kernel_variants_bit_identical(R, ctxs, golden_dir, case):
-    """Every render path (whole-traversal / dynamic-fetch megakernels, wavefront queues, tile
-    kernel, primary packets) gives the same bits and ray count, and matches the golden image."""
+    """Every render path (whole-traversal / dynamic-fetch kernels, each compiled variant, drain lane
+    groups and refill thresholds) gives the same bits and ray count, and matches the golden image."""
     name, cfg, W, H, uv, over = next(c for c in IMAGES if c[0] == case)
     g = golden(golden_dir)[name]
     _, ctx, prm, _, _ = ctxs(cfg, uv)
     prm = apply(R.rt_params.from_buffer_copy(prm), over)
     cam = R.camera_from_trackball(aspect=R.aspect_of(W, H))
-    keys = {k for v in KERNEL_VARIANTS for k in v}
-    saved = {k: os.environ.get(k) for k in keys}
-    try:
-        base = None
-        for v in KERNEL_VARIANTS:
-            for k in keys:
-                os.environ.pop(k, None)
-            os.environ.update(v)
+    base = None
+    for v in V.all_variants(R):
+        with V.options(R, ctx, v):
             img, st = ctx.render(cam, prm, W, H)
-            assert st.rays == int(g["rays"]), v
-            assert float(np.max(np.abs(img - g["img"]))) <= TOL, v
-            if base is None:
-                base = img
-            assert img.tobytes() == base.tobytes(), v
-    finally:
-        for k, val in saved.items():
-            if val is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = val
+        assert st.rays == int(g["rays"]), v
+        assert float(np.max(np.abs(img - g["img"]))) <= TOL, v
+        if base is None:
+            base = img
+        assert img.tobytes() == base.tobytes(), v
 
 
 @pytest.mark.parametrize("cfg,uv,kernel,aa", [("C2", None, "", 0), ("C2", None, "df", 0), ("C2", None, "df", 1),
                                               ("C3", (200, 80), "", 0), ("C4", (200, 80), "", 0),
                                               ("C5", None, "", 0)])
-def test_view_batch_bit_identical(R, O, ctxs, cfg, uv, kernel, aa, monkeypatch):
+def test_view_batch_bit_identical(R, O, ctxs, cfg, uv, kernel, aa):
     """rt_render_views_device: every view of a batch is bit-identical to rt_render_device with that
     camera (whole frame and band ranks; the batch runs its own refill / lane-group defaults), ray
     counts add up, and a rotated view matches the oracle."""
     import torch
 
-    if kernel:
-        monkeypatch.setenv("RT_KERNEL", kernel)
     scene, ctx, prm, _, _ = ctxs(cfg, uv)
+    opts = {R.OPT_KERNEL: R.KERNEL_DYNAMIC_FETCH} if kernel == "df" else {}
+    with V.options(R, ctx, opts):
+        _view_batch_checks(R, O, scene, ctx, prm, cfg, aa)
+
+
+def _view_batch_checks(R, O, scene, ctx, prm, cfg, aa):
+    import torch
+
     if aa:
         prm = type(prm).from_buffer_copy(prm)
         prm.anti_aliasing = 1

@@ -116,25 +116,21 @@ def test_oracle_texture_rules_and_filters(R, O, tmp_path):
     assert float(np.abs(imgs[(1, 2)] - imgs[(4, 2)]).max()) > 0.01
 
 
-def _compare_gpu(R, O, s, cases, W=48, H=32, kernels=("persistent", "df", "wavefront", "tile")):
+def _compare_gpu(R, O, s, cases, W=48, H=32, kernels=("whole", "df")):
+    import variants as V
+
     ctx = R.Context(s)
     o = O.Oracle(s)
     cam = R.camera_from_trackball(aspect=R.aspect_of(W, H))
-    saved = os.environ.get("RT_KERNEL")
-    try:
-        for p in cases:
-            ref, rays = o.render(p, W, H)
-            for k in kernels:
-                os.environ["RT_KERNEL"] = k
+    kinds = {"whole": R.KERNEL_WHOLE_TRAVERSAL, "df": R.KERNEL_DYNAMIC_FETCH}
+    for p in cases:
+        ref, rays = o.render(p, W, H)
+        for k in kernels:
+            with V.options(R, ctx, {R.OPT_KERNEL: kinds[k]}):
                 img, st = ctx.render(cam, p, W, H)
-                tag = (k, p.texture_filtering, p.out_of_bounds_x, p.out_of_bounds_y)
-                assert st.rays == rays, tag
-                assert float(np.max(np.abs(img - ref))) <= 1e-5, tag
-    finally:
-        if saved is None:
-            os.environ.pop("RT_KERNEL", None)
-        else:
-            os.environ["RT_KERNEL"] = saved
+            tag = (k, p.texture_filtering, p.out_of_bounds_x, p.out_of_bounds_y)
+            assert st.rays == rays, tag
+            assert float(np.max(np.abs(img - ref))) <= 1e-5, tag
     ctx.close()
 
 
@@ -150,7 +146,7 @@ def test_gpu_textures_every_filter_and_rule(R, O, tmp_path):
 def test_gpu_textures_reference_files(R, O, tmp_path, png):
     s = _textured_scene(R, str(tmp_path), png)
     cases = [_params(R, f, 2, 2) for f in (0, 1, 4)]
-    _compare_gpu(R, O, s, cases, kernels=("persistent", "df"))
+    _compare_gpu(R, O, s, cases, kernels=("whole", "df"))
 
 
 @pytest.mark.gpu

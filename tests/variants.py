@@ -1,0 +1,37 @@
+"""Render-path selection for the bit-identity tests: every compiled kernel variant and drain /
+refill setting of both kernel classes (rt_ctx_set_option; the library reads no environment)."""
+import contextlib
+
+
+def defaults(R):
+    return {R.OPT_KERNEL: R.KERNEL_AUTO, R.OPT_VARIANT: -1, R.OPT_COOP: -1, R.OPT_COOP_MAX: 0, R.OPT_REFILL: 0}
+
+
+def kernel_classes(R):
+    """The two shipped kernels, default variant each (textured and counting renders run these)."""
+    return [{R.OPT_KERNEL: R.KERNEL_WHOLE_TRAVERSAL}, {R.OPT_KERNEL: R.KERNEL_DYNAMIC_FETCH}]
+
+
+def all_variants(R):
+    wt, df = R.KERNEL_WHOLE_TRAVERSAL, R.KERNEL_DYNAMIC_FETCH
+    out = [{R.OPT_KERNEL: wt, R.OPT_VARIANT: v} for v in R.WT_VARIANTS]
+    out += [{R.OPT_KERNEL: df, R.OPT_VARIANT: v} for v in R.DF_VARIANTS]
+    out += [
+        {R.OPT_KERNEL: df, R.OPT_COOP: 0},                      # no drain lane groups
+        {R.OPT_KERNEL: df, R.OPT_COOP_MAX: 1},                  # drain groups of 64 lanes only
+        {R.OPT_KERNEL: df, R.OPT_COOP: 2, R.OPT_REFILL: 64},    # full-wave refill + straggler groups
+        {R.OPT_KERNEL: df, R.OPT_REFILL: 8},
+    ]
+    return out
+
+
+@contextlib.contextmanager
+def options(R, ctx, opts):
+    """Apply rt_ctx_set_option settings for the block, then restore the shipped defaults."""
+    try:
+        for k, v in opts.items():
+            ctx.set_option(k, v)
+        yield
+    finally:
+        for k, v in defaults(R).items():
+            ctx.set_option(k, v)

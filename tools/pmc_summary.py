@@ -6,10 +6,12 @@ Per counter: the median over the render-kernel dispatches of the per-dispatch va
 per launch follows MI355X_MICROARCH.md (HBM section): FETCH_SIZE and WRITE_SIZE are in KB;
 FETCH_SIZE counts 128-B requests at 64 B on gfx950, so it is doubled; WRITE_SIZE is exact.
 With --latest the summary is also written to profiles/pmc_latest.json, which bench.py reads for
-roofline.traffic.
+roofline.traffic -- only while `lib_sha` (sha256 of the librt_amd.so this tree ships, i.e. the build
+the GPU run profiled) matches the library bench.py loads.
 """
 import csv
 import glob
+import hashlib
 import json
 import os
 import statistics
@@ -43,7 +45,9 @@ def main():
     hbm = None
     if "FETCH_SIZE" in med and "WRITE_SIZE" in med:
         hbm = (2.0 * med["FETCH_SIZE"] + med["WRITE_SIZE"]) * 1024.0
-    d = {"config": cfg, "kernel": kname, "per_dispatch_median": med, "hbm_bytes_per_launch": hbm,
+    with open(os.path.join(REPO, "raytracer-group27_amd", "librt_amd.so"), "rb") as f:
+        sha = hashlib.sha256(f.read()).hexdigest()[:16]
+    d = {"config": cfg, "kernel": kname, "lib_sha": sha, "per_dispatch_median": med, "hbm_bytes_per_launch": hbm,
          "note": "rocprofv3 --pmc, one pass per counter group (tools/profile.sh); FETCH_SIZE/WRITE_SIZE in KB; "
                  "hbm_bytes_per_launch = (2*FETCH_SIZE + WRITE_SIZE)*1024 per MI355X_MICROARCH.md (gfx950 "
                  "FETCH_SIZE tallies 128-B requests at 64 B); Infinity-Cache hits are counted, not excluded"}

@@ -1,6 +1,7 @@
 """Developer tool: SIMD efficiency of the persistent kernels from the counting build.
 Per config and variant: lane node visits / (64 x wave node steps), same for triangle records
-and for state-machine advances (one per query).  Usage: python tools/simd_eff.py C3 old:RT_KERNEL=persistent df:
+and for state-machine advances (one per query).  Usage: python tools/simd_eff.py C3 whole:1=1 df:1=2
+(variant name : rt_ctx_set_option key=value pairs, e.g. 1=2 selects the dynamic-fetch kernel)
 SE_VIEWS=V renders a turntable batch of V views in one launch (rt_render_views_device) instead of one frame."""
 import os
 import sys
@@ -13,7 +14,6 @@ args = sys.argv[1:]
 cfgs = [a for a in args if a.startswith("C") and ":" not in a] or ["C3"]
 variants = [(a.split(":", 1)[0], dict(x.split("=") for x in a.split(":", 1)[1].split(",") if x))
             for a in args if ":" in a] or [("default", {})]
-keys = set(k for _, e in variants for k in e)
 for cfg in cfgs:
     s, p, W, H, desc = R.build_config(cfg)
     ctx = R.Context(s)
@@ -24,9 +24,10 @@ for cfg in cfgs:
         cams = R.turntable_cameras(V, R.aspect_of(W, H))
         buf = torch.zeros(V * R.local_band_elems(W, H, 8, 1), dtype=torch.float32, device="cuda")
     for name, env in variants:
-        for k in keys:
-            os.environ.pop(k, None)
-        os.environ.update(env)
+        for k, v in {R.OPT_KERNEL: 0, R.OPT_VARIANT: -1, R.OPT_COOP: -1, R.OPT_COOP_MAX: 0, R.OPT_REFILL: 0}.items():
+            ctx.set_option(k, v)
+        for k, v in env.items():
+            ctx.set_option(int(k), int(v))
         R.set_counting(True)
         if V > 1:
             st = ctx.render_views_device(cams, p, W, H, 8, 0, 1, buf.data_ptr(), None)

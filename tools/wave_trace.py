@@ -1,4 +1,4 @@
-"""Developer tool: per-wave timeline of the persistent render kernel (RT_WAVE_TRACE=1) -- launch
+"""Developer tool: per-wave timeline of the persistent render kernel (context option RT_OPT_WAVE_TRACE) -- launch
 skew, when each wave found the job queue empty, and what it did until it retired (drain
 iterations, tracing lanes per iteration, state-machine passes).
 Usage: python tools/wave_trace.py C3 [C4 ...]"""
@@ -12,7 +12,6 @@ import numpy as np  # noqa: E402
 
 import rt_amd as R  # noqa: E402
 
-os.environ["RT_WAVE_TRACE"] = "1"
 Q = [0, 1, 5, 25, 50, 75, 95, 99, 100]
 
 
@@ -23,6 +22,7 @@ def pct(x):
 for cfg in [a for a in sys.argv[1:] if a.startswith("C")] or ["C3"]:
     s, p, W, H, desc = R.build_config(cfg)
     ctx = R.Context(s)
+    ctx.set_option(R.OPT_WAVE_TRACE, 1)
     cam = R.camera_from_trackball(aspect=R.aspect_of(W, H))
     ctx.render(cam, p, W, H)
     _, st = ctx.render(cam, p, W, H)
