@@ -148,7 +148,9 @@ typedef struct rt_params {
     int out_of_bounds_x;          /* [RT_OOB_BORDER] outOfBoundsRuleX */
     int out_of_bounds_y;          /* [RT_OOB_BORDER] outOfBoundsRuleY */
     float border_color[3];        /* [0] textureBorderColor */
-    int pad_;
+    int shade_level;              /* rt_shade only: the recursion level of the given rays, getFinalColor's
+                                     `level` argument (src/main.cpp:129); renders ignore it (camera rays
+                                     are level 0) */
 } rt_params;
 
 /* TextureFiltering (src/image.h:22-29) */
@@ -220,6 +222,20 @@ int rt_scene_add_spot_light(rt_scene* scene, const rt_spot_light* l);
 int rt_scene_add_plane_light(rt_scene* scene, const rt_plane_light* l);
 int rt_scene_clear_lights(rt_scene* scene);
 int rt_scene_set_material(rt_scene* scene, int mesh, const rt_material* m);
+/* The meshes as loadMesh returns them (src/mesh.h:14-44): per mesh its vertices {p, n, texCoord},
+ * its triangles (vertex index triplets) and its material; `texture` indexes rt_scene_desc.textures
+ * (-1: none) and texture_path names the file.  Pointers stay valid until the scene is modified or
+ * freed. */
+typedef struct rt_mesh_view {
+    int num_vertices;
+    int num_triangles;
+    const float* vertices;      /* [num_vertices][8]: p.xyz, n.xyz, texCoord.xy */
+    const uint32_t* triangles;  /* [num_triangles][3] */
+    rt_material material;
+    const char* texture_path;   /* "" without a kd texture */
+} rt_mesh_view;
+int rt_scene_mesh_count(const rt_scene* scene, int* n);
+int rt_scene_mesh_get(const rt_scene* scene, int mesh, rt_mesh_view* out);
 /* Flat view (pointers stay valid until the scene is modified or freed). */
 int rt_scene_desc_get(const rt_scene* scene, rt_scene_desc* out);
 int rt_scene_free(rt_scene* scene);

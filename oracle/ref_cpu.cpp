@@ -973,7 +973,7 @@ int oracle_shade(oracle_scene* o, const rt_ray* rays, int n, const rt_params* P,
         r.t = rays[i].t;
         Counter cnt;
         cnt.pix = (uint32_t)i;
-        const V3 c = final_color(o->sc, *P, r, 0, cnt);
+        const V3 c = final_color(o->sc, *P, r, P->shade_level, cnt);  // getFinalColor(..., level)
         rgb[i * 3] = c.x;
         rgb[i * 3 + 1] = c.y;
         rgb[i * 3 + 2] = c.z;

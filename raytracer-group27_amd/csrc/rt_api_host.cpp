@@ -14,6 +14,7 @@
 struct rt_scene {
     rt::HostScene s;
     bool dirty = true;
+    std::vector<std::vector<float>> mesh_vertices;  // rt_scene_mesh_get views ([n][8] per mesh)
 };
 
 namespace rt {
@@ -128,6 +129,47 @@ extern "C" int rt_scene_set_material(rt_scene* sc, int mesh, const rt_material* 
     d.has_texture = m->has_texture != 0;
     d.texture = m->has_texture ? m->texture : -1;
     sc->dirty = true;
+    return RT_OK;
+}
+
+extern "C" int rt_scene_mesh_count(const rt_scene* sc, int* n) {
+    if (!sc || !n) return RT_ERR_INVALID;
+    *n = (int)sc->s.meshes.size();
+    return RT_OK;
+}
+
+extern "C" int rt_scene_mesh_get(const rt_scene* csc, int mesh, rt_mesh_view* out) {
+    if (!csc || !out || mesh < 0 || mesh >= (int)csc->s.meshes.size()) {
+        set_error("rt_scene_mesh_get: invalid argument");
+        return RT_ERR_INVALID;
+    }
+    rt_scene* sc = const_cast<rt_scene*>(csc);
+    if (sc->mesh_vertices.size() != sc->s.meshes.size()) sc->mesh_vertices.assign(sc->s.meshes.size(), {});
+    const Mesh& m = sc->s.meshes[mesh];
+    std::vector<float>& v = sc->mesh_vertices[mesh];
+    v.resize(m.vertices.size() * 8);
+    for (size_t i = 0; i < m.vertices.size(); ++i) {
+        const Vertex& x = m.vertices[i];
+        const float f[8] = {x.p.x, x.p.y, x.p.z, x.n.x, x.n.y, x.n.z, x.uv.x, x.uv.y};
+        std::memcpy(&v[i * 8], f, sizeof(f));
+    }
+    out->num_vertices = (int)m.vertices.size();
+    out->num_triangles = (int)m.triangles.size();
+    out->vertices = v.data();
+    out->triangles = m.triangles.empty() ? nullptr : m.triangles[0].data();
+    rt_material& r = out->material;
+    r = rt_material{};
+    r.kd[0] = m.material.kd.x;
+    r.kd[1] = m.material.kd.y;
+    r.kd[2] = m.material.kd.z;
+    r.ks[0] = m.material.ks.x;
+    r.ks[1] = m.material.ks.y;
+    r.ks[2] = m.material.ks.z;
+    r.shininess = m.material.shininess;
+    r.transparency = m.material.transparency;
+    r.has_texture = m.material.has_texture ? 1 : 0;
+    r.texture = m.material.texture;
+    out->texture_path = m.material.texture_path.c_str();
     return RT_OK;
 }
 

@@ -698,6 +698,7 @@ __device__ __forceinline__ bool start_job(const KParams& P, const JobSrc& J, Lan
     q.t = r.t;
     L.rpix = (uint32_t)job;
     new_tree(L);
+    L.level = P.shade_level;  // getFinalColor(scene, bvh, ray, level)
     return true;
 }
 

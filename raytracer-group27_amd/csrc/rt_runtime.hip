@@ -661,6 +661,10 @@ static int fill_params(rt_ctx* c, const rt_camera* cam, const rt_params* p, int 
         set_error("texture_filtering / out_of_bounds rule out of range");
         return RT_ERR_INVALID;
     }
+    if (p->shade_level < 0 || p->shade_level >= RT_MAX_DEPTH) {
+        set_error("shade_level must be in [0, 15]");
+        return RT_ERR_INVALID;
+    }
     if ((size_t)W * (size_t)H >= (size_t)1 << 32) {
         set_error("image too large (pixel ids are 32-bit)");
         return RT_ERR_INVALID;
@@ -674,6 +678,7 @@ static int fill_params(rt_ctx* c, const rt_camera* cam, const rt_params* p, int 
     K.S.tex_oob_y = p->out_of_bounds_y;
     for (int k = 0; k < 3; ++k) K.S.tex_border[k] = p->border_color[k];
     K.max_level = p->max_reflection_level;
+    K.shade_level = p->shade_level;
     K.glossy_n = p->glossy_ray_count;
     K.seed_lo = (uint32_t)(p->rng_seed & 0xFFFFFFFFull);
     K.seed_hi = (uint32_t)(p->rng_seed >> 32);

@@ -67,6 +67,12 @@ class rt_scene_desc(C.Structure):
                 ("textures", C.POINTER(rt_texture))]
 
 
+class rt_mesh_view(C.Structure):
+    """One mesh as loadMesh returns it (src/mesh.h:14-44): vertices [n][8] = p, n, texCoord."""
+    _fields_ = [("num_vertices", C.c_int), ("num_triangles", C.c_int), ("vertices", C.POINTER(C.c_float)),
+                ("triangles", C.POINTER(C.c_uint32)), ("material", rt_material), ("texture_path", C.c_char_p)]
+
+
 class rt_camera(C.Structure):
     _fields_ = [("position", C.c_float * 3), ("quat", C.c_float * 4), ("half_height", C.c_float),
                 ("half_width", C.c_float)]
@@ -79,7 +85,7 @@ class rt_params(C.Structure):
                 ("multiple_rays", C.c_int), ("sample_size", C.c_int), ("barycentric_mode", C.c_int),
                 ("rng_seed", C.c_uint64), ("use_textures", C.c_int), ("texture_filtering", C.c_int),
                 ("out_of_bounds_x", C.c_int), ("out_of_bounds_y", C.c_int), ("border_color", C.c_float * 3),
-                ("pad_", C.c_int)]
+                ("shade_level", C.c_int)]
 
 
 # TextureFiltering / OutOfBoundsRule (src/image.h:16-29)
@@ -123,7 +129,7 @@ EXPORTS = [
     "rt_set_counting", "rt_debug_counters", "rt_ctx_info", "rt_selftest_math",
     "rt_postprocess_device", "rt_bitmap_device", "rt_postprocess", "rt_bitmap", "rt_encode_bmp", "rt_write_bmp",
     "rt_philox4x32_10", "rt_debug_wave_trace", "rt_decode_png", "rt_ctx_set_option", "rt_texture_sample",
-    "rt_update_lights", "rt_update_materials", "rt_unpermute_views_device",
+    "rt_update_lights", "rt_update_materials", "rt_unpermute_views_device", "rt_scene_mesh_count", "rt_scene_mesh_get",
 ]
 
 # rt_ctx_set_option (include/rt_amd.h): test / developer hooks; defaults are the shipped path
@@ -236,6 +242,8 @@ def lib():
                                  P(rt_stats)], C.c_int),
             "rt_unpermute_bands_device": ([C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp], C.c_int),
             "rt_unpermute_views_device": ([C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp], C.c_int),
+            "rt_scene_mesh_count": ([vp, P(C.c_int)], C.c_int),
+            "rt_scene_mesh_get": ([vp, C.c_int, P(rt_mesh_view)], C.c_int),
             "rt_intersect": ([vp, vp, C.c_int, C.c_int, vp], C.c_int),
             "rt_shade": ([vp, vp, C.c_int, P(rt_params), P(C.c_float), P(C.c_uint64)], C.c_int),
             "rt_set_counting": ([C.c_int], C.c_int),
@@ -336,6 +344,22 @@ class Scene:
         d = rt_scene_desc()
         check(lib().rt_scene_desc_get(self.h, C.byref(d)), "rt_scene_desc_get")
         return d
+
+    def meshes(self):
+        """The meshes as loadMesh returns them: [(vertices [n][8] = p, n, texCoord), triangles [m][3],
+        rt_material, texture path)]."""
+        n = C.c_int()
+        check(lib().rt_scene_mesh_count(self.h, C.byref(n)))
+        out = []
+        for i in range(n.value):
+            v = rt_mesh_view()
+            check(lib().rt_scene_mesh_get(self.h, i, C.byref(v)), "rt_scene_mesh_get")
+            vert = np.ctypeslib.as_array(v.vertices, shape=(v.num_vertices * 8,)).reshape(-1, 8).copy() \
+                if v.num_vertices else np.zeros((0, 8), np.float32)
+            tri = np.ctypeslib.as_array(v.triangles, shape=(v.num_triangles * 3,)).reshape(-1, 3).copy() \
+                if v.num_triangles else np.zeros((0, 3), np.uint32)
+            out.append((vert, tri, rt_material.from_buffer_copy(v.material), v.texture_path.decode()))
+        return out
 
     def arrays(self):
         """numpy copies of the flat scene (positions [T,3,3], normals [T,3,3], mesh [T], materials)."""

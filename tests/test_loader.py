@@ -174,3 +174,22 @@ def test_dragon_proxy_deterministic(R, tmp_path):
     pos, nrm, _, mats = s.arrays()
     assert len(pos) == 2 * 40 * 16
     assert mats[0].shininess == 0.0 and list(mats[0].ks) == [0.5, 0.5, 0.5]
+
+
+@pytest.mark.parametrize("name,normalize", [("cube.obj", False), ("monkey-rotated.obj", True),
+                                            ("CornellBox-Mirror-Rotated.obj", True), ("tr_def.obj", False)])
+def test_mesh_view_matches_flat_scene(R, name, normalize):
+    """rt_scene_mesh_get (the facade's loadMesh data model: vertices + index triplets per mesh) flattens
+    mesh-major to exactly the scene-order triangles rt_create receives (loadObjectsFromScene,
+    src/bounding_volume_hierarchy.cpp:80-99)."""
+    s = R.Scene().load_obj(os.path.join(R.data_dir(), name), normalize=normalize)
+    pos, nrm, mesh, mats = s.arrays()
+    flat_p, flat_n, flat_m = [], [], []
+    for mi, (vert, tri, mat, _) in enumerate(s.meshes()):
+        assert mat.kd[:] == mats[mi].kd[:] and mat.shininess == mats[mi].shininess
+        flat_p.append(vert[tri][:, :, 0:3])
+        flat_n.append(vert[tri][:, :, 3:6])
+        flat_m.append(np.full(len(tri), mi))
+    assert np.concatenate(flat_p).astype(np.float32).tobytes() == pos.tobytes()
+    assert np.concatenate(flat_n).astype(np.float32).tobytes() == nrm.tobytes()
+    assert np.array_equal(np.concatenate(flat_m), mesh)
