@@ -274,9 +274,11 @@ int rt_render_device(rt_ctx* ctx, const rt_camera* cam, const rt_params* params,
  * capture) in ONE launch -- a sequence of renderRayTracing calls (src/main.cpp:340-400), one per
  * camera change of the trackball (framework/src/trackball.cpp:87-98).  The persistent job queue
  * spans every view, so the drain tail of one frame overlaps the start of the next.  d_rgb_out
- * holds n_views rt_render_device buffers back to back (view v at v * n_local_bands * band_rows *
- * width * 3 floats); view v's buffer is bit-identical to rt_render_device with cams[v].  Stats
- * are summed over the views.  n_views == 1 is rt_render_device.
+ * holds n_views rt_render_device buffers back to back, each padded to the band count of the
+ * busiest rank: view v at v * ceil(nbands / band_count) * band_rows * width * 3 floats, so the ranks'
+ * buffers gather into one array for rt_unpermute_views_device.  View v's bands are bit-identical to
+ * rt_render_device with cams[v].  Stats are summed over the views.  n_views == 1 is
+ * rt_render_device.
  */
 int rt_render_views_device(rt_ctx* ctx, const rt_camera* cams, int n_views, const rt_params* params,
                            int width, int height, int band_rows, int band_rank, int band_count,

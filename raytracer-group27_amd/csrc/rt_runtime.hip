@@ -853,7 +853,10 @@ extern "C" int rt_render_views_device(rt_ctx* c, const rt_camera* cams, int n_vi
     }
     K.out = d_out;
     K.n_views = n_views;
-    K.view_rows = K.n_local_bands * band_rows;
+    // views are spaced by the padded band count every rank has (ceil(nbands / band_count)), so the
+    // band_count ranks' buffers gather into one [rank][view][band][row] array whatever rank renders
+    // fewer bands (rt_unpermute_views_device)
+    K.view_rows = ((nbands + band_count - 1) / band_count) * band_rows;
     std::vector<float> v((size_t)n_views * 12, 0.0f);
     for (int i = 0; i < n_views; ++i) {
         float* o = v.data() + 12 * i;
