@@ -798,14 +798,17 @@ __device__ __attribute__((noinline)) bool advance_lane_call(const KParams& P, co
     return advance_lane<COUNT, TEX>(P, J, L, fr, hit, b, q, cnt, job_rays);
 }
 
-// Kernel variants (compile-time): bit 0 RT_V_CALL = state machine out of line; bit 1 RT_V_NOPF = no
-// node prefetch in the dynamic-fetch traversal; bit 2 RT_V_NOCOOP = no drain lane groups; bit 3
-// RT_V_W3 = compiled for 3 waves per SIMD (168 VGPRs) instead of 2 (256).  Every variant renders the
-// same bits; they differ in registers, spills and occupancy.
+// Kernel variants (compile-time): bit 0 RT_V_CALL = state machine (and the drain lane groups) out of
+// line; bit 1 RT_V_NOPF = no node prefetch in the dynamic-fetch traversal; bit 2 RT_V_NOCOOP = no drain
+// lane groups; bit 3 RT_V_W3 / bit 4 RT_V_W4 = compiled for 3 / 4 waves per SIMD (168 / 128 VGPRs)
+// instead of 2 (256).  Every variant renders the same bits; they differ in registers, spills and
+// occupancy.
 #define RT_V_CALL 1
 #define RT_V_NOPF 2
 #define RT_V_NOCOOP 4
 #define RT_V_W3 8
+#define RT_V_W4 16  // compiled for 4 waves per SIMD (128 VGPRs)
+#define RT_V_WAVES(V) (((V) & RT_V_W4) ? 4 : (((V) & RT_V_W3) ? 3 : 2))
 
 template <bool COUNT, bool TEX, int V>
 __device__ __forceinline__ bool advance_v(const KParams& P, const JobSrc& J, Lane& L, Frame* fr, bool hit, const Best& b,
@@ -818,7 +821,7 @@ __device__ __forceinline__ bool advance_v(const KParams& P, const JobSrc& J, Lan
 // Refill between whole traversals: every busy lane traces its query with trace_query8, then
 // advances; idle lanes take jobs (one atomic per wave).
 template <bool COUNT, bool TEX, int V>
-__global__ __launch_bounds__(64, (V & RT_V_W3) ? 3 : 2) void persistent_kernel(KParams P, JobSrc J) {
+__global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_kernel(KParams P, JobSrc J) {
     __shared__ int stack_lds[RT_STACK_SIZE * RT_WAVE];
     __shared__ int s_base;
     const int lane_id = threadIdx.x;
@@ -1072,7 +1075,7 @@ __device__ __forceinline__ void trav_record(const DevScene& S, Trav& T, Cnt& cnt
 // the owner's arithmetic (tri_test, leaf_reachable) against the group's running best; the best
 // is the lexicographic minimum of (t, key) and an any-hit query takes any accepted candidate, so
 // every owner ends with the hit its own walk would give (tests/test_gpu_parity.py, RT_COOP=0 vs 1).
-#define COOP_POOL 2048  // node groups, split between the lane groups
+#define COOP_POOL 1024  // node groups, split between the lane groups (4 KB: with the 4-KB stack, 16 blocks fit a CU)
 #define COOP_Q 16       // queries one drain traversal takes
 
 // query hand-over through LDS: [field][COOP_Q]
@@ -1349,6 +1352,17 @@ __device__ __forceinline__ uint2 coop_group_trace(const float4* __restrict__ nod
     return n;
 }
 
+// The drain traversal as an out-of-line call (RT_V_CALL variants): its registers are the callee's,
+// not added to the traversal loop's.
+template <int NW>
+__device__ __attribute__((noinline)) uint2 coop_group_trace_call(const float4* __restrict__ nodes,
+                                                                 const float4* __restrict__ tri,
+                                                                 const DRefNode* __restrict__ refn,
+                                                                 const int* __restrict__ leaf_path, int* pool, int* q,
+                                                                 unsigned long long om, int reserve) {
+    return coop_group_trace<NW>(nodes, tri, refn, leaf_path, pool, q, om, reserve);
+}
+
 // Epilogue of trace_query8: the spheres, after every triangle (same order and keys).
 __device__ __forceinline__ void trav_finish(const DevScene& S, Trav& T) {
     if (T.any && T.found) return;
@@ -1368,7 +1382,7 @@ __device__ __forceinline__ void trav_finish(const DevScene& S, Trav& T) {
 }
 
 template <bool COUNT, bool TEX, int V>
-__global__ __launch_bounds__(64, (V & RT_V_W3) ? 3 : 2) void persistent_df_kernel(KParams P, JobSrc J) {
+__global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParams P, JobSrc J) {
     constexpr bool PF = !(V & RT_V_NOPF), COOP = !(V & RT_V_NOCOOP);
     __shared__ int stack_lds[RT_STACK8 * RT_WAVE];
     __shared__ int coop_pool[COOP_POOL];   // drain: node groups of the wave's last queries
@@ -1497,8 +1511,12 @@ __global__ __launch_bounds__(64, (V & RT_V_W3) ? 3 : 2) void persistent_df_kerne
                         if (T.cur != RT_TRAV_NONE) gp[T.sp] = (int)T.cur;
                     }
                     __syncthreads();
-                    const uint2 nv = coop_group_trace<8>(S.nodes, S.tri, S.refn, S.leaf_path, coop_pool, coop_q, om,
-                                                         P.coop_reserve);
+                    const uint2 nv =
+                        (V & RT_V_CALL)
+                            ? coop_group_trace_call<8>(S.nodes, S.tri, S.refn, S.leaf_path, coop_pool, coop_q, om,
+                                                       P.coop_reserve)
+                            : coop_group_trace<8>(S.nodes, S.tri, S.refn, S.leaf_path, coop_pool, coop_q, om,
+                                                  P.coop_reserve);
                     __syncthreads();
                     if (COUNT) {
                         cnt.nodes += nv.x;

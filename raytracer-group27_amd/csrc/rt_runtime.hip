@@ -43,8 +43,9 @@ struct rt_ctx {
     int nnodes = 0, nrec = 0, ntri = 0, nmesh = 0;
     int ref_nodes = 0, ref_levels = 0;
     int bvh8_depth = 0;
+    bool df_ok = true;  // the BVH8 fits the dynamic-fetch kernel's LDS stack
     bool glossy_material = false;  // opaque, ks > 0, shininess != 0 (glossy_ray_count > 1 draws lobes)
-    int persistent_blocks[32] = {0};  // resident 64-lane blocks per (kernel class, variant)
+    int persistent_blocks[64] = {0};  // resident 64-lane blocks per (kernel class, variant)
     // lights (re-uploadable: rt_update_lights)
     void* d_lights[4] = {nullptr, nullptr, nullptr, nullptr};
     // developer wave trace (RT_OPT_WAVE_TRACE)
@@ -60,7 +61,7 @@ struct rt_ctx {
     int opt_coop_max = 0;   // 0: the largest count the LDS pool allows
     int opt_refill = 0;     // 0: per render shape
     int opt_wave_trace = 0;
-    int opt_variant = -1;   // -1: the class default (RT_DF_DEFAULT / RT_WT_DEFAULT)
+    int opt_variant = -1;   // -1: the shipped variant for the render shape (RT_DF_BATCH / _FRAME, RT_WT_DEFAULT)
     char last_kernel[64] = {0};
 };
 
@@ -345,7 +346,8 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
         return RT_ERR_INVALID;
     }
     c->bvh8_depth = bvh8.max_depth;
-    if (bvh8.max_depth + 2 >= RT_STACK8 || (int)bvh8.order.size() != ntri) {
+    c->df_ok = bvh8.max_depth + 2 < RT_STACK8;  // else the whole-traversal kernel's deeper stack
+    if (bvh8.max_depth + 2 >= RT_STACK_SIZE || (int)bvh8.order.size() != ntri) {
         set_error("rt_create: BVH8 deeper than the traversal stack");
         delete c;
         return RT_ERR_INVALID;
@@ -503,7 +505,7 @@ extern "C" int rt_ctx_set_option(rt_ctx* c, int option, int value) {
     switch (option) {
         case RT_OPT_KERNEL:
             if (value < RT_KERNEL_AUTO || value > RT_KERNEL_DYNAMIC_FETCH) break;
-            if (value == RT_KERNEL_DYNAMIC_FETCH && c->bvh8_depth + 2 >= RT_STACK8) {
+            if (value == RT_KERNEL_DYNAMIC_FETCH && !c->df_ok) {
                 set_error("rt_ctx_set_option: BVH8 too deep for the dynamic-fetch kernel's stack");
                 return RT_ERR_INVALID;
             }
@@ -525,7 +527,7 @@ extern "C" int rt_ctx_set_option(rt_ctx* c, int option, int value) {
             c->opt_wave_trace = value ? 1 : 0;
             return RT_OK;
         case RT_OPT_VARIANT:
-            if (value < -1 || value > 15) break;
+            if (value < -1 || value > 31) break;
             c->opt_variant = value;
             return RT_OK;
         default:
@@ -539,21 +541,27 @@ extern "C" int rt_ctx_set_option(rt_ctx* c, int option, int value) {
 
 // the kernel class a render runs: whole-traversal refill for small scenes, dynamic fetch for large
 static bool use_df(const rt_ctx* c) {
-    if (c->opt_kernel == RT_KERNEL_WHOLE_TRAVERSAL) return false;
+    if (!c->df_ok || c->opt_kernel == RT_KERNEL_WHOLE_TRAVERSAL) return false;
     if (c->opt_kernel == RT_KERNEL_DYNAMIC_FETCH) return true;
     return c->ntri >= RT_DF_MIN_TRIANGLES;
 }
 
-// Kernel variants compiled (rt_megakernel.hip RT_V_*): the shipped default of each class first, then
-// the alternatives kept for A/B measurement (RT_OPT_VARIANT; all render identical bits).
-#define RT_DF_DEFAULT (RT_V_CALL | RT_V_NOPF)
+// Kernel variants compiled (rt_megakernel.hip RT_V_*).  The dynamic-fetch class ships two, chosen by
+// render shape: view batches run the lean 3-waves-per-SIMD variant (state machine
+// out of line, no node prefetch, no drain lane groups: C3 16 views 1.21 -> 0.96 ms/frame, C4 25.3 ->
+// 18.3 ms/frame), single frames the 2-wave variant with the drain lane groups (their tail dominates:
+// C3 2.19 vs 2.46 ms).  The rest are kept for A/B measurement (RT_OPT_VARIANT); all render identical bits.
+#define RT_DF_BATCH (RT_V_CALL | RT_V_NOPF | RT_V_NOCOOP | RT_V_W3)
+#define RT_DF_FRAME 0
 #define RT_WT_DEFAULT (RT_V_CALL | RT_V_W3)
-static const int kDfVariants[] = {RT_DF_DEFAULT, 0, RT_V_CALL, RT_V_CALL | RT_V_NOPF | RT_V_NOCOOP | RT_V_W3};
-static const int kWtVariants[] = {RT_WT_DEFAULT, 0};
+#define RT_DF_ALT1 (RT_V_CALL | RT_V_NOPF | RT_V_W3)
+#define RT_DF_ALT2 (RT_V_CALL | RT_V_NOPF | RT_V_NOCOOP | RT_V_W4)
+#define RT_DF_ALT3 (RT_V_CALL | RT_V_NOPF | RT_V_W4)
 
-static int variant_of(const rt_ctx* c, bool df) {
+static int variant_of(const rt_ctx* c, bool df, int n_views) {
     if (c->opt_variant >= 0) return c->opt_variant;
-    return df ? RT_DF_DEFAULT : RT_WT_DEFAULT;
+    if (!df) return RT_WT_DEFAULT;
+    return n_views > 1 ? RT_DF_BATCH : RT_DF_FRAME;
 }
 
 template <bool COUNT, bool TEX, int V>
@@ -564,35 +572,33 @@ static void launch_v(bool df, int grid, hipStream_t st, const KParams& K, const 
         hipLaunchKernelGGL((persistent_kernel<COUNT, TEX, V>), dim3(grid), dim3(64), 0, st, K, J);
 }
 
+// every (COUNT, TEX) instance of the shipped variants; the A/B alternates plain only
+template <bool COUNT, bool TEX>
+static bool launch_shipped(bool df, int v, int grid, hipStream_t st, const KParams& K, const JobSrc& J) {
+    if (df && v == RT_DF_BATCH) launch_v<COUNT, TEX, RT_DF_BATCH>(true, grid, st, K, J);
+    else if (df && v == RT_DF_FRAME) launch_v<COUNT, TEX, RT_DF_FRAME>(true, grid, st, K, J);
+    else if (!df && v == RT_WT_DEFAULT) launch_v<COUNT, TEX, RT_WT_DEFAULT>(false, grid, st, K, J);
+    else return false;
+    return true;
+}
+
 template <bool COUNT>
 static int launch_persistent(int grid, hipStream_t st, const KParams& K, const JobSrc& J, rt_ctx* c) {
     const bool df = use_df(c);
     const bool tex = COUNT || K.S.tex_on;  // counting builds keep the texture code (one instance each)
-    const int v = variant_of(c, df);
-    const int dv = df ? RT_DF_DEFAULT : RT_WT_DEFAULT;
-    if (COUNT || tex) {
-        if (v != dv) {
-            set_error("kernel variant: counting and textured renders exist in the default variant only");
-            return RT_ERR_INVALID;
-        }
-        if (df) launch_v<COUNT, true, RT_DF_DEFAULT>(true, grid, st, K, J);
-        else launch_v<COUNT, true, RT_WT_DEFAULT>(false, grid, st, K, J);
-    } else if (df) {
-        switch (v) {
-            case RT_DF_DEFAULT: launch_v<false, false, RT_DF_DEFAULT>(true, grid, st, K, J); break;
-            case 0: launch_v<false, false, 0>(true, grid, st, K, J); break;
-            case RT_V_CALL: launch_v<false, false, RT_V_CALL>(true, grid, st, K, J); break;
-            case RT_V_CALL | RT_V_NOPF | RT_V_NOCOOP | RT_V_W3:
-                launch_v<false, false, RT_V_CALL | RT_V_NOPF | RT_V_NOCOOP | RT_V_W3>(true, grid, st, K, J);
-                break;
-            default: set_error("kernel variant not compiled"); return RT_ERR_INVALID;
-        }
-    } else {
-        switch (v) {
-            case RT_WT_DEFAULT: launch_v<false, false, RT_WT_DEFAULT>(false, grid, st, K, J); break;
-            case 0: launch_v<false, false, 0>(false, grid, st, K, J); break;
-            default: set_error("kernel variant not compiled"); return RT_ERR_INVALID;
-        }
+    const int v = variant_of(c, df, K.n_views);
+    bool ok = tex ? launch_shipped<COUNT, true>(df, v, grid, st, K, J) : launch_shipped<COUNT, false>(df, v, grid, st, K, J);
+    if (!ok && !COUNT && !tex) {
+        ok = true;
+        if (df && v == RT_DF_ALT1) launch_v<false, false, RT_DF_ALT1>(true, grid, st, K, J);
+        else if (df && v == RT_DF_ALT2) launch_v<false, false, RT_DF_ALT2>(true, grid, st, K, J);
+        else if (df && v == RT_DF_ALT3) launch_v<false, false, RT_DF_ALT3>(true, grid, st, K, J);
+        else if (!df && v == 0) launch_v<false, false, 0>(false, grid, st, K, J);
+        else ok = false;
+    }
+    if (!ok) {
+        set_error("kernel variant not compiled for this render (counting and textured renders: shipped variants only)");
+        return RT_ERR_INVALID;
     }
     // the name rocprofv3 lists for this launch (bench.py's roofline.kernel)
     std::snprintf(c->last_kernel, sizeof(c->last_kernel), "rt::%s<%s, %s, %d>",
@@ -608,19 +614,20 @@ static int occupancy_of(int* per_cu) {
 }
 
 // resident 64-lane blocks of the kernel (the persistent grid)
-static int persistent_grid(rt_ctx* c) {
+static int persistent_grid(rt_ctx* c, int n_views) {
     const bool df = use_df(c);
-    const int v = variant_of(c, df);
-    const int key = (df ? 16 : 0) + (v & 15);
+    const int v = variant_of(c, df, n_views);
+    const int key = (df ? 32 : 0) + (v & 31);
     if (c->persistent_blocks[key] > 0) return c->persistent_blocks[key];
     int cus = 0, per_cu = 0;
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
     int e = 1;
     if (df) {
-        if (v == RT_DF_DEFAULT) e = occupancy_of<true, RT_DF_DEFAULT>(&per_cu);
-        else if (v == 0) e = occupancy_of<true, 0>(&per_cu);
-        else if (v == RT_V_CALL) e = occupancy_of<true, RT_V_CALL>(&per_cu);
-        else e = occupancy_of<true, RT_V_CALL | RT_V_NOPF | RT_V_NOCOOP | RT_V_W3>(&per_cu);
+        if (v == RT_DF_BATCH) e = occupancy_of<true, RT_DF_BATCH>(&per_cu);
+        else if (v == RT_DF_FRAME) e = occupancy_of<true, RT_DF_FRAME>(&per_cu);
+        else if (v == RT_DF_ALT1) e = occupancy_of<true, RT_DF_ALT1>(&per_cu);
+        else if (v == RT_DF_ALT2) e = occupancy_of<true, RT_DF_ALT2>(&per_cu);
+        else e = occupancy_of<true, RT_DF_ALT3>(&per_cu);
     } else {
         if (v == RT_WT_DEFAULT) e = occupancy_of<false, RT_WT_DEFAULT>(&per_cu);
         else e = occupancy_of<false, 0>(&per_cu);
@@ -765,7 +772,7 @@ static int launch_render(rt_ctx* c, KParams& K, hipStream_t st, int count_mode, 
         K.view_jobs = J.view_jobs;
         J.counter = reinterpret_cast<int*>(c->d_stats + 7);
         J.xq = use_df(c) ? reinterpret_cast<int*>(c->d_stats + 16) : nullptr;
-        const int grid = (int)std::min<long long>(blocks * J.n_views, persistent_grid(c));
+        const int grid = (int)std::min<long long>(blocks * J.n_views, persistent_grid(c, K.n_views));
         if (c->opt_wave_trace) {
             const int rc = ensure(c, &c->d_wave_trace, &c->wave_trace_bytes, (size_t)grid * 8 * 8);
             if (rc != RT_OK) return rc;
@@ -1018,7 +1025,7 @@ extern "C" int rt_shade(rt_ctx* c, const rt_ray* rays, int n, const rt_params* p
         J.view_jobs = n;
         J.counter = reinterpret_cast<int*>(c->d_stats + 7);
         J.xq = use_df(c) ? reinterpret_cast<int*>(c->d_stats + 16) : nullptr;
-        const int grid = std::min((n + 63) / 64, persistent_grid(c));
+        const int grid = std::min((n + 63) / 64, persistent_grid(c, 1));
         if (launch_persistent<false>(grid, c->stream, K, J, c) != RT_OK) e = hipErrorInvalidValue;
         else e = hipGetLastError();
     }
