@@ -550,13 +550,16 @@ static bool use_df(const rt_ctx* c) {
 // render shape: view batches run the lean 3-waves-per-SIMD variant (state machine
 // out of line, no node prefetch, no drain lane groups: C3 16 views 1.21 -> 0.96 ms/frame, C4 25.3 ->
 // 18.3 ms/frame), single frames the 2-wave variant with the drain lane groups (their tail dominates:
-// C3 2.19 vs 2.46 ms).  The rest are kept for A/B measurement (RT_OPT_VARIANT); all render identical bits.
+// C3 2.25 vs 2.27-2.76 ms, C4 45.6 vs 48-58 ms).  The whole-traversal class (small scenes) keeps the
+// inline 2-wave variant (C2 0.76 vs 0.81 ms, C5 742 vs 804 ms).  The rest are kept for A/B
+// measurement (RT_OPT_VARIANT); all render identical bits.
 #define RT_DF_BATCH (RT_V_CALL | RT_V_NOPF | RT_V_NOCOOP | RT_V_W3)
 #define RT_DF_FRAME 0
-#define RT_WT_DEFAULT (RT_V_CALL | RT_V_W3)
-#define RT_DF_ALT1 (RT_V_CALL | RT_V_NOPF | RT_V_W3)
-#define RT_DF_ALT2 (RT_V_CALL | RT_V_NOPF | RT_V_NOCOOP | RT_V_W4)
+#define RT_WT_DEFAULT 0
+#define RT_DF_ALT1 (RT_V_CALL | RT_V_NOPF | RT_V_NOCOOP | RT_V_W4)
+#define RT_DF_ALT2 (RT_V_CALL | RT_V_NOPF | RT_V_W3)
 #define RT_DF_ALT3 (RT_V_CALL | RT_V_NOPF | RT_V_W4)
+#define RT_WT_ALT1 (RT_V_CALL | RT_V_W3)
 
 static int variant_of(const rt_ctx* c, bool df, int n_views) {
     if (c->opt_variant >= 0) return c->opt_variant;
@@ -593,7 +596,7 @@ static int launch_persistent(int grid, hipStream_t st, const KParams& K, const J
         if (df && v == RT_DF_ALT1) launch_v<false, false, RT_DF_ALT1>(true, grid, st, K, J);
         else if (df && v == RT_DF_ALT2) launch_v<false, false, RT_DF_ALT2>(true, grid, st, K, J);
         else if (df && v == RT_DF_ALT3) launch_v<false, false, RT_DF_ALT3>(true, grid, st, K, J);
-        else if (!df && v == 0) launch_v<false, false, 0>(false, grid, st, K, J);
+        else if (!df && v == RT_WT_ALT1) launch_v<false, false, RT_WT_ALT1>(false, grid, st, K, J);
         else ok = false;
     }
     if (!ok) {
@@ -630,7 +633,7 @@ static int persistent_grid(rt_ctx* c, int n_views) {
         else e = occupancy_of<true, RT_DF_ALT3>(&per_cu);
     } else {
         if (v == RT_WT_DEFAULT) e = occupancy_of<false, RT_WT_DEFAULT>(&per_cu);
-        else e = occupancy_of<false, 0>(&per_cu);
+        else e = occupancy_of<false, RT_WT_ALT1>(&per_cu);
     }
     if (e != 0 || per_cu <= 0) per_cu = 8;
     c->persistent_blocks[key] = std::max(1, cus) * per_cu;

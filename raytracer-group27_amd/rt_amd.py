@@ -138,8 +138,8 @@ KERNEL_AUTO, KERNEL_WHOLE_TRAVERSAL, KERNEL_DYNAMIC_FETCH = 0, 1, 2
 # compiled kernel variants (rt_megakernel.hip RT_V_*, rt_runtime.hip kDfVariants / kWtVariants)
 V_CALL, V_NOPF, V_NOCOOP, V_W3, V_W4 = 1, 2, 4, 8, 16
 DF_BATCH, DF_FRAME = V_CALL | V_NOPF | V_NOCOOP | V_W3, 0  # shipped dynamic-fetch variants (by render shape)
-DF_VARIANTS = [DF_BATCH, DF_FRAME, V_CALL | V_NOPF | V_W3, V_CALL | V_NOPF | V_NOCOOP | V_W4, V_CALL | V_NOPF | V_W4]
-WT_VARIANTS = [V_CALL | V_W3, 0]
+DF_VARIANTS = [DF_BATCH, DF_FRAME, V_CALL | V_NOPF | V_NOCOOP | V_W4, V_CALL | V_NOPF | V_W3, V_CALL | V_NOPF | V_W4]
+WT_VARIANTS = [0, V_CALL | V_W3]
 
 class rt_post_params(C.Structure):
     """Screen post-processing settings (src/screen.h:58-111), raw setter values."""
