@@ -8,7 +8,7 @@ void set_error(const std::string& msg);
 
 #define RT_MAX_DEPTH 16        // frames of the recursion stack (reference default depth 5, configs <= 8)
 #define RT_STACK_SIZE 40       // BVH2 traversal stack entries per lane (BVH depth <= 37, bvh_build.cpp)
-#define RT_STACK8 16           // dynamic-fetch kernel: BVH8 group-stack entries per lane (BVH8 depth <= 13;
+#define RT_STACK8 12           // dynamic-fetch kernel: BVH8 group-stack entries per lane (BVH8 depth <= 13;
                                // the 800k-triangle dragon proxy has depth 7); deeper trees run the whole-traversal kernel
 #define RT_MAX_REF_NODES 31    // depth-4 binary reference BVH
 #define RT_WAVE 64

@@ -28,30 +28,53 @@ struct Query {
     float t;  // initial ray.t: FLT_MAX, or the caller's ray.t for rt_shade's explicit rays
 };
 
+struct JobSrc;
+
+// The render kernels' own arguments (KParams, then JobSrc), read through the kernarg segment pointer
+// `ka` the kernel passes down.  The out-of-line parts of the state machine use these instead of
+// reference parameters: a reference to a kernel argument makes the compiler copy the 400-B KParams
+// into every lane's private memory and read it back with vector loads; through the (uniform) segment
+// pointer the reads are scalar loads.
+__device__ __forceinline__ const char* uniform_kernarg(const void* ka) {
+    typedef const __attribute__((address_space(4))) char* CB;
+    const uint64_t a = (uint64_t)ka;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    return (const char*)(CB)(((uint64_t)hi << 32) | lo);
+}
+
+__device__ __forceinline__ const KParams& kernel_params(const void* ka) {
+    return *(const KParams*)uniform_kernarg(ka);
+}
+
 // Per-lane state between queries: the pixel, the position in the recursion tree and in the light
-// loop of the current shading point.  Kept small: it is live across every traversal step.
+// loop of the current shading point.  Kept small (39 dwords without textures): it is live across
+// every traversal step.
 struct Lane {
     int job;        // >= 0 job index; -1 idle (fetch another); -2 no more work
     uint32_t rpix;  // the reference's pixel id y * W + x (rt_shade: the ray index), glossy Philox counter
-    int out_row;    // row of the pixel in the band buffer
-    int sample;     // camera sample (AA / getPixelRays)
-    int level;      // recursion level of the current node
-    int nfr;        // pending frames (transparent / glossy branches)
-    bool desc;      // the current node descends to its mirror / reflected child after its lights
-    bool shadow;    // the query in flight is a cansee segment
-    v3 pacc;        // pixel: sum of the finished camera samples
+    uint32_t sample : 7;  // camera sample (AA / getPixelRays: < 64)
+    uint32_t level : 5;   // recursion level of the current node (<= RT_MAX_DEPTH)
+    uint32_t nfr : 5;     // pending frames (transparent / glossy branches, <= RT_MAX_DEPTH)
+    uint32_t lt : 3;      // light loop: type (LType)
+    uint32_t desc : 1;    // the current node descends to its mirror / reflected child after its lights
+    uint32_t shadow : 1;  // the query in flight is a cansee segment
+    int li : 16, ls : 16; // light loop: index, sample (-1: before the first; fill_params bounds both)
     v3 acc;         // current camera sample: forward-accumulated colour
     v3 w, wc;       // weight of the current node / of its mirror or reflected child
-    v3 hp, nN, nR, refl;  // shading point: hitPoint, normalize(normal), normalize(reflect), reflect
+    v3 hp, nN, refl;  // shading point: hitPoint, normalize(normal), reflect (nR = normalize(refl))
     int mat;        // >= 0 mesh material, < 0: sphere -(s+1)
     v3 color;       // direct light of the current node
-    int lt, li, ls; // light loop: type, index, sample
     float a0, a1, a2, a3;  // per-light accumulators
     v3 u0, u1;             // spherical light: perp | plane light: (px, py)
     float sdist, sI;       // cansee: remaining distance, intensity
     uint32_t draws;        // glossy: Philox draws of this camera sample
-    v3 kd;                 // TEX kernels: kd of the shading point (texture or material)
+    v3 kd;                 // TEX kernels only: kd of the shading point (texture or material)
 };
+
+static_assert(sizeof(Lane) == 42 * 4, "Lane layout (39 dwords + the TEX kernels' kd)");
+
+__device__ __forceinline__ v3 lane_nR(const Lane& L) { return normalize(L.refl); }
 
 __device__ __forceinline__ DMat load_mat(const DevScene& S, int m) {
     if (m >= 0) return S.mats[m];
@@ -252,7 +275,7 @@ __device__ __forceinline__ bool start_cansee(Lane& L, v3 target, Query& q) {
 __device__ __forceinline__ void light_cos(const Lane& L, v3 lp, float& cosL, float& cosS) {
     const v3 ldir = normalize(lp - L.hp);
     cosL = fabsf(dot(L.nN, ldir));
-    const float d2 = dot(L.nR, ldir);
+    const float d2 = dot(lane_nR(L), ldir);
     cosS = (0.0f < d2) ? d2 : 0.0f;
 }
 
@@ -275,7 +298,7 @@ __device__ __forceinline__ v3 sphere_perp(const Lane& L, v3 lp, float radius) {
 // in q) or every light is done (false).  `vis` is the result of the cansee that just finished
 // (valid when have_result).
 template <bool TEX>
-__device__ bool advance_lights(const KParams& P, Lane& L, bool have_result, bool vis, Query& q) {
+__device__ __forceinline__ bool advance_lights_body(const KParams& P, Lane& L, bool have_result, bool vis, Query& q) {
     const DevScene& S = P.S;
     for (;;) {
         if (L.lt == L_POINT) {
@@ -407,7 +430,7 @@ __device__ bool advance_lights(const KParams& P, Lane& L, bool have_result, bool
                     const float dn = dot(normalize(L.hp - px), normal);
                     L.a0 += ((dn < 0.0f) ? 0.0f : dn) / length(L.hp - px);
                     L.a1 += 1.0f;
-                    const float c2 = dot(L.nR, normalize(px - L.hp));
+                    const float c2 = dot(lane_nR(L), normalize(px - L.hp));
                     L.a2 = (L.a2 < c2) ? c2 : L.a2;
                 }
                 const v3 dx = (1.0f / (float)(k - 1)) * w;
@@ -438,13 +461,21 @@ __device__ bool advance_lights(const KParams& P, Lane& L, bool have_result, bool
     }
 }
 
+// the light loop as its own function: fewer live registers in the caller
+template <bool TEX>
+__device__ __attribute__((noinline)) bool advance_lights_call(const void* ka, Lane& L, bool have_result, bool vis,
+                                                              Query& q) {
+    return advance_lights_body<TEX>(kernel_params(ka), L, have_result, vis, q);
+}
+
+
 // ---- recursion tree ------------------------------------------------------------------------
 // Next lobe sample of the glossy frame f (src/main.cpp:209-249): two uniforms per draw from the
 // Philox stream (key = rng_seed, counter = (draw, pixel, sample, 0)) in place of rand(); up to
 // glossy_ray_count / 4 redraws while the direction points into the surface.  Returns true with the
 // sample ray in q and its lobe weight max(pow(dot(reflect, dir), shininess), 0) in cw; false when
 // the lobe is done.
-__device__ bool glossy_next(const KParams& P, Lane& L, Frame& f, Query& q, float& cw) {
+__device__ __forceinline__ bool glossy_next_body(const KParams& P, Lane& L, Frame& f, Query& q, float& cw) {
     const v3 r = f.d;
     v3 notr = r;
     if (r.x != 0.0f) {
@@ -483,6 +514,10 @@ __device__ bool glossy_next(const KParams& P, Lane& L, Frame& f, Query& q, float
     return false;
 }
 
+__device__ __attribute__((noinline)) bool glossy_next_call(const void* ka, Lane& L, Frame& f, Query& q, float& cw) {
+    return glossy_next_body(kernel_params(ka), L, f, q, cw);
+}
+
 // A getFinalColor node was hit by the path query (qo, qd): record the shading point, start its
 // light loop and decide its children (src/main.cpp:131-290) -- the mirror or reflected child after
 // the lights (L.desc, weight L.wc), and a frame for a pending refracted ray or a glossy lobe.
@@ -498,7 +533,6 @@ __device__ __forceinline__ void begin_node(const KParams& P, Lane& L, Frame* fr,
     L.hp = s.p;
     L.nN = normalize(s.n);
     L.refl = reflect(normalize(qd), L.nN);
-    L.nR = normalize(L.refl);
     L.mat = (b.rec >= 0) ? s.mesh : b.rec;
     if (TEX) L.kd = v3{s.m.kd[0], s.m.kd[1], s.m.kd[2]};
     L.color = v3{0.0f, 0.0f, 0.0f};
@@ -557,7 +591,7 @@ __device__ __forceinline__ void begin_node(const KParams& P, Lane& L, Frame* fr,
 
 // The subtree under the current node is finished: resume the deepest pending branch (true, query
 // in q) or report the camera sample complete (false, colour in L.acc).
-__device__ __forceinline__ bool next_branch(const KParams& P, Lane& L, Frame* fr, Query& q) {
+__device__ __forceinline__ bool next_branch(const KParams& P, const void* ka, Lane& L, Frame* fr, Query& q) {
     while (L.nfr > 0) {
         Frame& f = fr[L.nfr - 1];
         if (f.mode == FR_REFRACT) {
@@ -570,7 +604,7 @@ __device__ __forceinline__ bool next_branch(const KParams& P, Lane& L, Frame* fr
             return true;
         }
         float cw;
-        if (glossy_next(P, L, f, q, cw)) {  // reflectColor += child * cw (src/main.cpp:239-240)
+        if (glossy_next_call(ka, L, f, q, cw)) {  // reflectColor += child * cw (src/main.cpp:239-240)
             L.level = f.level;
             L.w = f.w * cw;
             return true;
@@ -593,6 +627,12 @@ struct JobSrc {
     int n_views;    // view batch: njobs = n_views * view_jobs
     int view_jobs;  // jobs of one view (a multiple of 64)
 };
+
+// the second kernel argument of the render kernels (see kernel_params)
+__device__ __forceinline__ const JobSrc& kernel_jobs(const void* ka) {
+    constexpr size_t off = (sizeof(KParams) + alignof(JobSrc) - 1) / alignof(JobSrc) * alignof(JobSrc);
+    return *(const JobSrc*)(uniform_kernarg(ka) + off);
+}
 
 // Job range of XCD group x: a contiguous run of 8x8 tiles (a horizontal band of the frame), so
 // the rays of one XCD touch the geometry of one band and its L2 holds that part of the scene.
@@ -622,8 +662,11 @@ __device__ __forceinline__ void new_tree(Lane& L) {
     L.w = v3{1.0f, 1.0f, 1.0f};
     L.level = 0;
     L.nfr = 0;
+    L.lt = L_POINT;
+    L.desc = false;
     L.draws = 0u;
     L.shadow = false;
+    L.sdist = 0.0f;
 }
 
 // queue the camera ray of the lane's current sample (src/main.cpp:350-386)
@@ -649,16 +692,19 @@ __device__ __forceinline__ void queue_camera(const KParams& P, Lane& L, Query& q
         sx = ndx + (P.ms_offx * qx * (float)xx);
         sy = ndy + (P.ms_offy * qy * (float)yy);
     }
-    if (P.n_views > 1)
-        gen_ray_view(P, L.out_row / P.view_rows, sx, sy, q.o, q.d);
-    else
+    if (P.n_views > 1) {
+        int view;
+        view_job(P, L.job, view);
+        gen_ray_view(P, view, sx, sy, q.o, q.d);
+    } else
         gen_ray(P, sx, sy, q.o, q.d);
     q.t = FLT_MAX;
     new_tree(L);
 }
 
-// Map a job index to its pixel (8x8 tiles inside the rank's bands).  False if outside the image.
-__device__ __forceinline__ bool job_pixel(const KParams& P, int gjob, Lane& L) {
+// Map a job index to its pixel (8x8 tiles inside the rank's bands): the reference's pixel id and the
+// pixel's row in the band buffer.  False if outside the image.
+__device__ __forceinline__ bool job_pixel(const KParams& P, int gjob, uint32_t& rpix, int& out_row) {
     int view;
     const int job = view_job(P, gjob, view);
     const int tiles_x = (P.W + 7) / 8;
@@ -673,8 +719,8 @@ __device__ __forceinline__ bool job_pixel(const KParams& P, int gjob, Lane& L) {
     const int row_in_band = ty * 8 + (lane >> 3);
     const int px = tx * 8 + (lane & 7);
     const int py = gb * P.band_rows + row_in_band;
-    L.rpix = (uint32_t)(py * P.W + px);  // the reference's pixel (x, y), y up
-    L.out_row = view * P.view_rows + lb * P.band_rows + row_in_band;
+    rpix = (uint32_t)(py * P.W + px);  // the reference's pixel (x, y), y up
+    out_row = view * P.view_rows + lb * P.band_rows + row_in_band;
     return (px < P.W) && (row_in_band < P.band_rows) && (py < P.H) && (lb < P.n_local_bands);
 }
 
@@ -683,9 +729,9 @@ __device__ __forceinline__ bool job_pixel(const KParams& P, int gjob, Lane& L) {
 __device__ __forceinline__ bool start_job(const KParams& P, const JobSrc& J, Lane& L, int job, Query& q) {
     L.job = job;
     L.sample = 0;
-    L.pacc = v3{0.0f, 0.0f, 0.0f};
     if (J.mode == 0) {
-        if (!job_pixel(P, job, L)) {
+        int out_row;
+        if (!job_pixel(P, job, L.rpix, out_row)) {
             L.job = -1;
             return false;
         }
@@ -707,7 +753,7 @@ __device__ __forceinline__ bool start_job(const KParams& P, const JobSrc& J, Lan
 // output.  Returns true with the next query in q (L.shadow says which kind); false when the lane's
 // job is complete (L.job = -1).
 template <bool COUNT, bool TEX>
-__device__ __forceinline__ bool advance_lane(const KParams& P, const JobSrc& J, Lane& L, Frame* fr, bool hit, const Best& b,
+__device__ __forceinline__ bool advance_lane(const KParams& P, const JobSrc& J, const void* ka, Lane& L, Frame* fr, bool hit, const Best& b,
                              Query& q, Cnt& cnt, uint32_t job_rays) {
     const DevScene& S = P.S;
     bool lights_have = false, lights_vis = false;
@@ -744,7 +790,7 @@ __device__ __forceinline__ bool advance_lane(const KParams& P, const JobSrc& J, 
     bool more;
     if (L.shadow || hit) {
         L.shadow = false;
-        if (advance_lights<TEX>(P, L, lights_have, lights_vis, q)) return true;
+        if (advance_lights_call<TEX>(ka, L, lights_have, lights_vis, q)) return true;
         // every light done: the node's colour, then its mirror / reflected child
         L.acc = L.acc + L.w * L.color;
         if (L.desc) {
@@ -755,30 +801,33 @@ __device__ __forceinline__ bool advance_lane(const KParams& P, const JobSrc& J, 
             q.t = FLT_MAX;
             return true;
         }
-        more = next_branch(P, L, fr, q);
+        more = next_branch(P, ka, L, fr, q);
     } else {
-        more = next_branch(P, L, fr, q);  // a miss: getFinalColor returns black
+        more = next_branch(P, ka, L, fr, q);  // a miss: getFinalColor returns black
     }
     if (more) return true;
-    // camera sample complete
+    // camera sample complete: the pixel's samples are summed in its output slot, in sample order
     if (J.mode == 0) {
-        if (P.aa || P.multi) L.pacc += L.acc;
-        else L.pacc = L.acc;
-        L.sample++;
+        uint32_t rpix;
+        int out_row;
+        job_pixel(P, L.job, rpix, out_row);
+        const int px = (int)(rpix % (uint32_t)P.W);
+        float* dst = P.out + ((size_t)out_row * P.W + px) * 3;
         const int nsamples = P.aa ? 4 : (P.multi ? P.sample_size : 1);
+        v3 col = L.acc;
+        if (nsamples > 1) {
+            const v3 sum = (L.sample == 0) ? v3{0.0f, 0.0f, 0.0f} : v3{dst[0], dst[1], dst[2]};
+            col = sum + L.acc;
+            if (L.sample + 1 == nsamples) col = P.aa ? col * 0.25f : col * (float)(1.0f / (float)P.sample_size);
+        }
+        dst[0] = col.x;
+        dst[1] = col.y;
+        dst[2] = col.z;
+        L.sample++;
         if (L.sample < nsamples) {
             queue_camera(P, L, q);
             return true;
         }
-        v3 col = L.pacc;
-        if (P.aa) col = L.pacc * 0.25f;
-        else if (P.multi) col = L.pacc * (float)(1.0f / (float)P.sample_size);
-        const int py = (int)(L.rpix / (uint32_t)P.W);
-        const int px = (int)(L.rpix - (uint32_t)py * (uint32_t)P.W);
-        float* dst = P.out + ((size_t)L.out_row * P.W + px) * 3;
-        dst[0] = col.x;
-        dst[1] = col.y;
-        dst[2] = col.z;
     } else {
         J.rgb[L.job * 3 + 0] = L.acc.x;
         J.rgb[L.job * 3 + 1] = L.acc.y;
@@ -792,14 +841,12 @@ __device__ __forceinline__ bool advance_lane(const KParams& P, const JobSrc& J, 
 // The same advance as an out-of-line call: the lane's state then lives in the call's private frame
 // between queries instead of in registers across the traversal loop (kernel variant bit RT_V_CALL).
 template <bool COUNT, bool TEX>
-__device__ __attribute__((noinline)) bool advance_lane_call(const KParams& P, const JobSrc& J, Lane& L, Frame* fr,
-                                                            bool hit, const Best& b, Query& q, Cnt& cnt,
-                                                            uint32_t job_rays) {
-    return advance_lane<COUNT, TEX>(P, J, L, fr, hit, b, q, cnt, job_rays);
+__device__ __attribute__((noinline)) bool advance_lane_call(const void* ka, Lane& L, Frame* fr, bool hit, const Best& b,
+                                                            Query& q, Cnt& cnt, uint32_t job_rays) {
+    return advance_lane<COUNT, TEX>(kernel_params(ka), kernel_jobs(ka), ka, L, fr, hit, b, q, cnt, job_rays);
 }
 
-// Kernel variants (compile-time): bit 0 RT_V_CALL = state machine (and the drain lane groups) out of
-// line; bit 1 RT_V_NOPF = no node prefetch in the dynamic-fetch traversal; bit 2 RT_V_NOCOOP = no drain
+// Kernel variants (compile-time): bit 0 RT_V_CALL = state machine out of line (with RT_V_NOCOOP); bit 1 RT_V_NOPF = no node prefetch in the dynamic-fetch traversal; bit 2 RT_V_NOCOOP = no drain
 // lane groups; bit 3 RT_V_W3 / bit 4 RT_V_W4 = compiled for 3 / 4 waves per SIMD (168 / 128 VGPRs)
 // instead of 2 (256).  Every variant renders the same bits; they differ in registers, spills and
 // occupancy.
@@ -808,13 +855,15 @@ __device__ __attribute__((noinline)) bool advance_lane_call(const KParams& P, co
 #define RT_V_NOCOOP 4
 #define RT_V_W3 8
 #define RT_V_W4 16  // compiled for 4 waves per SIMD (128 VGPRs)
-#define RT_V_WAVES(V) (((V) & RT_V_W4) ? 4 : (((V) & RT_V_W3) ? 3 : 2))
+#define RT_V_W5 128  // compiled for 5 waves per SIMD (~100 VGPRs)
+#define RT_V_WAVES(V) (((V) & RT_V_W5) ? 5 : ((V) & RT_V_W4) ? 4 : (((V) & RT_V_W3) ? 3 : 2))
+
 
 template <bool COUNT, bool TEX, int V>
-__device__ __forceinline__ bool advance_v(const KParams& P, const JobSrc& J, Lane& L, Frame* fr, bool hit, const Best& b,
-                                          Query& q, Cnt& cnt, uint32_t job_rays) {
-    if (V & RT_V_CALL) return advance_lane_call<COUNT, TEX>(P, J, L, fr, hit, b, q, cnt, job_rays);
-    return advance_lane<COUNT, TEX>(P, J, L, fr, hit, b, q, cnt, job_rays);
+__device__ __forceinline__ bool advance_v(const KParams& P, const JobSrc& J, const void* ka, Lane& L, Frame* fr,
+                                          bool hit, const Best& b, Query& q, Cnt& cnt, uint32_t job_rays) {
+    if constexpr ((V & RT_V_CALL) != 0) return advance_lane_call<COUNT, TEX>(ka, L, fr, hit, b, q, cnt, job_rays);
+    else return advance_lane<COUNT, TEX>(P, J, ka, L, fr, hit, b, q, cnt, job_rays);
 }
 
 // ---- whole-traversal persistent kernel ------------------------------------------------------
@@ -826,6 +875,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_kernel(KParams P
     __shared__ int s_base;
     const int lane_id = threadIdx.x;
     int* stk = stack_lds + lane_id;
+    const void* ka = (const void*)__builtin_amdgcn_kernarg_segment_ptr();  // this kernel's (P, J)
     const unsigned long long t_wave0 = P.wave_trace ? wall_clock64() : 0ull;
     unsigned int wave_jobs = 0;  // jobs this wave took (wave trace)
     const DevScene& S = P.S;
@@ -876,7 +926,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_kernel(KParams P
         if (!busy) continue;
         if (COUNT && wave_leader()) cnt.wadv++;
         // ---- advance the state machine until the next query ----
-        need_trace = advance_v<COUNT, TEX, V>(P, J, L, fr, hit, b, q, cnt, job_rays);
+        need_trace = advance_v<COUNT, TEX, V>(P, J, ka, L, fr, hit, b, q, cnt, job_rays);
     }
     flush_counters<COUNT>(P, cnt);
     if (P.wave_trace && lane_id == 0) {  // wave trace: (start, end, jobs) per wave, 100 MHz clock
@@ -1352,17 +1402,6 @@ __device__ __forceinline__ uint2 coop_group_trace(const float4* __restrict__ nod
     return n;
 }
 
-// The drain traversal as an out-of-line call (RT_V_CALL variants): its registers are the callee's,
-// not added to the traversal loop's.
-template <int NW>
-__device__ __attribute__((noinline)) uint2 coop_group_trace_call(const float4* __restrict__ nodes,
-                                                                 const float4* __restrict__ tri,
-                                                                 const DRefNode* __restrict__ refn,
-                                                                 const int* __restrict__ leaf_path, int* pool, int* q,
-                                                                 unsigned long long om, int reserve) {
-    return coop_group_trace<NW>(nodes, tri, refn, leaf_path, pool, q, om, reserve);
-}
-
 // Epilogue of trace_query8: the spheres, after every triangle (same order and keys).
 __device__ __forceinline__ void trav_finish(const DevScene& S, Trav& T) {
     if (T.any && T.found) return;
@@ -1383,13 +1422,16 @@ __device__ __forceinline__ void trav_finish(const DevScene& S, Trav& T) {
 
 template <bool COUNT, bool TEX, int V>
 __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParams P, JobSrc J) {
-    constexpr bool PF = !(V & RT_V_NOPF), COOP = !(V & RT_V_NOCOOP);
+    // the drain lane groups run inline only: with the out-of-line state machine (RT_V_CALL) the variant
+    // is compiled without them (an out-of-line drain call there lost values the kernel held across it)
+    constexpr bool PF = !(V & RT_V_NOPF), COOP = !(V & (RT_V_NOCOOP | RT_V_CALL));
     __shared__ int stack_lds[RT_STACK8 * RT_WAVE];
     __shared__ int coop_pool[COOP_POOL];   // drain: node groups of the wave's last queries
     __shared__ int coop_q[CQ_N * COOP_Q];  // drain: those queries
     __shared__ int s_base, s_lim;
     const int lane_id = threadIdx.x;
     int* stk = stack_lds + lane_id;
+    const void* ka = (const void*)__builtin_amdgcn_kernarg_segment_ptr();  // this kernel's (P, J)
     const unsigned long long t_wave0 = P.wave_trace ? wall_clock64() : 0ull;
     unsigned int wave_jobs = 0;  // jobs this wave took (wave trace)
     const DevScene& S = P.S;
@@ -1419,7 +1461,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
             if (COUNT && wave_leader()) cnt.wadv++;
             q.o = T.o;
             q.d = T.d;
-            start = advance_v<COUNT, TEX, V>(P, J, L, fr, T.found, T.best, q, cnt, job_rays);
+            start = advance_v<COUNT, TEX, V>(P, J, ka, L, fr, T.found, T.best, q, cnt, job_rays);
         }
         const unsigned long long tJ = COUNT ? (unsigned long long)clock64() : 0ull;
         if (COUNT) cnt.cyc_c += tJ - tA;  // state machine
@@ -1511,12 +1553,8 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
                         if (T.cur != RT_TRAV_NONE) gp[T.sp] = (int)T.cur;
                     }
                     __syncthreads();
-                    const uint2 nv =
-                        (V & RT_V_CALL)
-                            ? coop_group_trace_call<8>(S.nodes, S.tri, S.refn, S.leaf_path, coop_pool, coop_q, om,
-                                                       P.coop_reserve)
-                            : coop_group_trace<8>(S.nodes, S.tri, S.refn, S.leaf_path, coop_pool, coop_q, om,
-                                                  P.coop_reserve);
+                    const uint2 nv = coop_group_trace<8>(S.nodes, S.tri, S.refn, S.leaf_path, coop_pool, coop_q, om,
+                                                         P.coop_reserve);
                     __syncthreads();
                     if (COUNT) {
                         cnt.nodes += nv.x;

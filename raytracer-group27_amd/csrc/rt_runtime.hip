@@ -45,7 +45,7 @@ struct rt_ctx {
     int bvh8_depth = 0;
     bool df_ok = true;  // the BVH8 fits the dynamic-fetch kernel's LDS stack
     bool glossy_material = false;  // opaque, ks > 0, shininess != 0 (glossy_ray_count > 1 draws lobes)
-    int persistent_blocks[64] = {0};  // resident 64-lane blocks per (kernel class, variant)
+    int persistent_blocks[512] = {0};  // resident 64-lane blocks per (kernel class, variant)
     // lights (re-uploadable: rt_update_lights)
     void* d_lights[4] = {nullptr, nullptr, nullptr, nullptr};
     // developer wave trace (RT_OPT_WAVE_TRACE)
@@ -527,7 +527,7 @@ extern "C" int rt_ctx_set_option(rt_ctx* c, int option, int value) {
             c->opt_wave_trace = value ? 1 : 0;
             return RT_OK;
         case RT_OPT_VARIANT:
-            if (value < -1 || value > 31) break;
+            if (value < -1 || value > 255) break;
             c->opt_variant = value;
             return RT_OK;
         default:
@@ -547,18 +547,18 @@ static bool use_df(const rt_ctx* c) {
 }
 
 // Kernel variants compiled (rt_megakernel.hip RT_V_*).  The dynamic-fetch class ships two, chosen by
-// render shape: view batches run the lean 3-waves-per-SIMD variant (state machine
-// out of line, no node prefetch, no drain lane groups: C3 16 views 1.21 -> 0.96 ms/frame, C4 25.3 ->
-// 18.3 ms/frame), single frames the 2-wave variant with the drain lane groups (their tail dominates:
-// C3 2.25 vs 2.27-2.76 ms, C4 45.6 vs 48-58 ms).  The whole-traversal class (small scenes) keeps the
-// inline 2-wave variant (C2 0.76 vs 0.81 ms, C5 742 vs 804 ms).  The rest are kept for A/B
-// measurement (RT_OPT_VARIANT); all render identical bits.
-#define RT_DF_BATCH (RT_V_CALL | RT_V_NOPF | RT_V_NOCOOP | RT_V_W3)
+// render shape: view batches run the lean 4-waves-per-SIMD variant (state machine
+// out of line, no node prefetch, no drain lane groups: C3 16 views 0.785 ms/frame vs 0.907 at 3 waves,
+// 0.99 at 5, 1.11 for the 2-wave frame variant; C4 14.96 vs 17.8 / 18.7 / 24.1 ms/frame), single
+// frames the 2-wave variant with the drain lane groups (their tail dominates: C3 2.16-2.19 vs
+// 2.29-2.67 ms).  The whole-traversal class (small scenes) keeps the inline 2-wave variant (C2 0.76 vs
+// 0.81 ms, C5 742 vs 804 ms).  The alternates are kept for A/B measurement (RT_OPT_VARIANT); all
+// render identical bits.
+#define RT_DF_BATCH (RT_V_CALL | RT_V_NOPF | RT_V_NOCOOP | RT_V_W4)
 #define RT_DF_FRAME 0
 #define RT_WT_DEFAULT 0
-#define RT_DF_ALT1 (RT_V_CALL | RT_V_NOPF | RT_V_NOCOOP | RT_V_W4)
-#define RT_DF_ALT2 (RT_V_CALL | RT_V_NOPF | RT_V_W3)
-#define RT_DF_ALT3 (RT_V_CALL | RT_V_NOPF | RT_V_W4)
+#define RT_DF_ALT1 (RT_V_CALL | RT_V_NOPF | RT_V_NOCOOP | RT_V_W3)
+#define RT_DF_ALT2 (RT_V_CALL | RT_V_NOPF | RT_V_NOCOOP | RT_V_W5)
 #define RT_WT_ALT1 (RT_V_CALL | RT_V_W3)
 
 static int variant_of(const rt_ctx* c, bool df, int n_views) {
@@ -567,9 +567,9 @@ static int variant_of(const rt_ctx* c, bool df, int n_views) {
     return n_views > 1 ? RT_DF_BATCH : RT_DF_FRAME;
 }
 
-template <bool COUNT, bool TEX, int V>
-static void launch_v(bool df, int grid, hipStream_t st, const KParams& K, const JobSrc& J) {
-    if (df)
+template <bool DF, bool COUNT, bool TEX, int V>
+static void launch_v(int grid, hipStream_t st, const KParams& K, const JobSrc& J) {
+    if constexpr (DF)
         hipLaunchKernelGGL((persistent_df_kernel<COUNT, TEX, V>), dim3(grid), dim3(64), 0, st, K, J);
     else
         hipLaunchKernelGGL((persistent_kernel<COUNT, TEX, V>), dim3(grid), dim3(64), 0, st, K, J);
@@ -578,9 +578,9 @@ static void launch_v(bool df, int grid, hipStream_t st, const KParams& K, const 
 // every (COUNT, TEX) instance of the shipped variants; the A/B alternates plain only
 template <bool COUNT, bool TEX>
 static bool launch_shipped(bool df, int v, int grid, hipStream_t st, const KParams& K, const JobSrc& J) {
-    if (df && v == RT_DF_BATCH) launch_v<COUNT, TEX, RT_DF_BATCH>(true, grid, st, K, J);
-    else if (df && v == RT_DF_FRAME) launch_v<COUNT, TEX, RT_DF_FRAME>(true, grid, st, K, J);
-    else if (!df && v == RT_WT_DEFAULT) launch_v<COUNT, TEX, RT_WT_DEFAULT>(false, grid, st, K, J);
+    if (df && v == RT_DF_BATCH) launch_v<true, COUNT, TEX, RT_DF_BATCH>(grid, st, K, J);
+    else if (df && v == RT_DF_FRAME) launch_v<true, COUNT, TEX, RT_DF_FRAME>(grid, st, K, J);
+    else if (!df && v == RT_WT_DEFAULT) launch_v<false, COUNT, TEX, RT_WT_DEFAULT>(grid, st, K, J);
     else return false;
     return true;
 }
@@ -593,10 +593,9 @@ static int launch_persistent(int grid, hipStream_t st, const KParams& K, const J
     bool ok = tex ? launch_shipped<COUNT, true>(df, v, grid, st, K, J) : launch_shipped<COUNT, false>(df, v, grid, st, K, J);
     if (!ok && !COUNT && !tex) {
         ok = true;
-        if (df && v == RT_DF_ALT1) launch_v<false, false, RT_DF_ALT1>(true, grid, st, K, J);
-        else if (df && v == RT_DF_ALT2) launch_v<false, false, RT_DF_ALT2>(true, grid, st, K, J);
-        else if (df && v == RT_DF_ALT3) launch_v<false, false, RT_DF_ALT3>(true, grid, st, K, J);
-        else if (!df && v == RT_WT_ALT1) launch_v<false, false, RT_WT_ALT1>(false, grid, st, K, J);
+        if (df && v == RT_DF_ALT1) launch_v<true, false, false, RT_DF_ALT1>(grid, st, K, J);
+        else if (df && v == RT_DF_ALT2) launch_v<true, false, false, RT_DF_ALT2>(grid, st, K, J);
+        else if (!df && v == RT_WT_ALT1) launch_v<false, false, false, RT_WT_ALT1>(grid, st, K, J);
         else ok = false;
     }
     if (!ok) {
@@ -612,15 +611,17 @@ static int launch_persistent(int grid, hipStream_t st, const KParams& K, const J
 
 template <bool DF, int V>
 static int occupancy_of(int* per_cu) {
-    if (DF) return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, persistent_df_kernel<false, false, V>, 64, 0);
-    return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, persistent_kernel<false, false, V>, 64, 0);
+    if constexpr (DF)
+        return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, persistent_df_kernel<false, false, V>, 64, 0);
+    else
+        return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, persistent_kernel<false, false, V>, 64, 0);
 }
 
 // resident 64-lane blocks of the kernel (the persistent grid)
 static int persistent_grid(rt_ctx* c, int n_views) {
     const bool df = use_df(c);
     const int v = variant_of(c, df, n_views);
-    const int key = (df ? 32 : 0) + (v & 31);
+    const int key = (df ? 256 : 0) + (v & 255);
     if (c->persistent_blocks[key] > 0) return c->persistent_blocks[key];
     int cus = 0, per_cu = 0;
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
@@ -629,8 +630,7 @@ static int persistent_grid(rt_ctx* c, int n_views) {
         if (v == RT_DF_BATCH) e = occupancy_of<true, RT_DF_BATCH>(&per_cu);
         else if (v == RT_DF_FRAME) e = occupancy_of<true, RT_DF_FRAME>(&per_cu);
         else if (v == RT_DF_ALT1) e = occupancy_of<true, RT_DF_ALT1>(&per_cu);
-        else if (v == RT_DF_ALT2) e = occupancy_of<true, RT_DF_ALT2>(&per_cu);
-        else e = occupancy_of<true, RT_DF_ALT3>(&per_cu);
+        else e = occupancy_of<true, RT_DF_ALT2>(&per_cu);
     } else {
         if (v == RT_WT_DEFAULT) e = occupancy_of<false, RT_WT_DEFAULT>(&per_cu);
         else e = occupancy_of<false, RT_WT_ALT1>(&per_cu);
@@ -673,6 +673,14 @@ static int fill_params(rt_ctx* c, const rt_camera* cam, const rt_params* p, int 
     }
     if (p->shade_level < 0 || p->shade_level >= RT_MAX_DEPTH) {
         set_error("shade_level must be in [0, 15]");
+        return RT_ERR_INVALID;
+    }
+    // the state machine's light cursor holds light index and sample in 16-bit fields
+    // (rt_megakernel.hip Lane::li / ls)
+    const int nl_max = std::max(std::max(c->S.npl, c->S.nsl), std::max(c->S.nspot, c->S.nplane));
+    if (nl_max >= 32767 || (long long)p->sphere_light_ray_count >= 32767 ||
+        (long long)p->plane_light_1D_ray_count * p->plane_light_1D_ray_count >= 32767) {
+        set_error("more than 32766 lights of one kind or light samples per light");
         return RT_ERR_INVALID;
     }
     if ((size_t)W * (size_t)H >= (size_t)1 << 32) {
