@@ -99,6 +99,7 @@ struct KParams {
     unsigned long long* stats;  // rays, node visits, tri tests, hits, ..., UB-regime hits
     int refill;                 // dynamic-fetch kernel: waiting lanes that end a traversal phase
     int shade_level;            // rt_shade: recursion level of the explicit rays (getFinalColor's `level`)
+    int fan;                    // dynamic-fetch kernel: spherical-light samples traced as wave-shared fans
     uint32_t seed_lo, seed_hi;  // glossy sampling: Philox-4x32-10 key (rt_params.rng_seed)
     unsigned long long* wave_trace;  // developer wave trace (rt_ctx_set_option RT_OPT_WAVE_TRACE), or null
     int coop;                        // dynamic-fetch kernel: lane-group traversal of the drain's queries

@@ -280,8 +280,8 @@ __device__ __forceinline__ void light_cos(const Lane& L, v3 lp, float& cosL, flo
 }
 
 // getSpherelights' first perp (src/shadow.cpp:160-175)
-__device__ __forceinline__ v3 sphere_perp(const Lane& L, v3 lp, float radius) {
-    v3 dd = normalize(lp - L.hp);
+__device__ __forceinline__ v3 sphere_perp(v3 hp, v3 lp, float radius) {
+    v3 dd = normalize(lp - hp);
     v3 notd = dd;
     if (dd.x != 0.0f) {
         notd.y = -dd.x;
@@ -298,7 +298,8 @@ __device__ __forceinline__ v3 sphere_perp(const Lane& L, v3 lp, float radius) {
 // in q) or every light is done (false).  `vis` is the result of the cansee that just finished
 // (valid when have_result).
 template <bool TEX>
-__device__ __forceinline__ bool advance_lights_body(const KParams& P, Lane& L, bool have_result, bool vis, Query& q) {
+__device__ __forceinline__ bool advance_lights_body(const KParams& P, Lane& L, bool have_result, bool vis,
+                                                    uint64_t fanvis, Query& q) {
     const DevScene& S = P.S;
     for (;;) {
         if (L.lt == L_POINT) {
@@ -333,10 +334,18 @@ __device__ __forceinline__ bool advance_lights_body(const KParams& P, Lane& L, b
             const v3 lp = ld3(sl.position);
             if (have_result) {
                 have_result = false;
-                if (L.ls == -1) {
+                if (L.ls == -2) {
+                    // the whole fan, traced by the wave (fan_sample_query): bit s of fanvis = sample s
+                    // visible, bit 0 the centre.  Opaque scene: every intensity is 1, so the loop's sums
+                    // below are these integer counts (exact in float)
+                    const float nv = (float)__popcll(fanvis >> 1);
+                    L.a0 = 1.0f + nv;
+                    L.a1 = (float)(fanvis & 1ull) + nv;
+                    L.ls = P.sl_m * P.sl_n;
+                } else if (L.ls == -1) {
                     L.a0 = L.sI;  // intensitySum is the centre sample's intensity (mutated even if blocked)
                     L.a1 = vis ? 1.0f : 0.0f;
-                    L.u0 = sphere_perp(L, lp, sl.radius);
+                    L.u0 = sphere_perp(L.hp, lp, sl.radius);
                     L.ls = 0;
                 } else {
                     if (vis) {
@@ -360,6 +369,13 @@ __device__ __forceinline__ bool advance_lights_body(const KParams& P, Lane& L, b
                 L.li++;
                 L.ls = -1;
                 continue;
+            }
+            if (L.ls == -1 && P.fan) {
+                // fan request: the kernel traces the centre and every sample of this light from hp
+                // across the wave's lanes and resumes here with the visibility mask
+                L.ls = -2;
+                L.shadow = true;
+                return true;
             }
             v3 target = lp;
             if (L.ls >= 0) {
@@ -464,8 +480,8 @@ __device__ __forceinline__ bool advance_lights_body(const KParams& P, Lane& L, b
 // the light loop as its own function: fewer live registers in the caller
 template <bool TEX>
 __device__ __attribute__((noinline)) bool advance_lights_call(const void* ka, Lane& L, bool have_result, bool vis,
-                                                              Query& q) {
-    return advance_lights_body<TEX>(kernel_params(ka), L, have_result, vis, q);
+                                                              uint64_t fanvis, Query& q) {
+    return advance_lights_body<TEX>(kernel_params(ka), L, have_result, vis, fanvis, q);
 }
 
 
@@ -753,8 +769,9 @@ __device__ __forceinline__ bool start_job(const KParams& P, const JobSrc& J, Lan
 // output.  Returns true with the next query in q (L.shadow says which kind); false when the lane's
 // job is complete (L.job = -1).
 template <bool COUNT, bool TEX>
-__device__ __forceinline__ bool advance_lane(const KParams& P, const JobSrc& J, const void* ka, Lane& L, Frame* fr, bool hit, const Best& b,
-                             Query& q, Cnt& cnt, uint32_t job_rays) {
+__device__ __forceinline__ bool advance_lane(const KParams& P, const JobSrc& J, const void* ka, Lane& L, Frame* fr,
+                                             bool hit, const Best& b, uint64_t fanvis, Query& q, Cnt& cnt,
+                                             uint32_t job_rays) {
     const DevScene& S = P.S;
     bool lights_have = false, lights_vis = false;
     if (L.shadow) {
@@ -790,7 +807,7 @@ __device__ __forceinline__ bool advance_lane(const KParams& P, const JobSrc& J, 
     bool more;
     if (L.shadow || hit) {
         L.shadow = false;
-        if (advance_lights_call<TEX>(ka, L, lights_have, lights_vis, q)) return true;
+        if (advance_lights_call<TEX>(ka, L, lights_have, lights_vis, fanvis, q)) return true;
         // every light done: the node's colour, then its mirror / reflected child
         L.acc = L.acc + L.w * L.color;
         if (L.desc) {
@@ -842,8 +859,8 @@ __device__ __forceinline__ bool advance_lane(const KParams& P, const JobSrc& J, 
 // between queries instead of in registers across the traversal loop (kernel variant bit RT_V_CALL).
 template <bool COUNT, bool TEX>
 __device__ __attribute__((noinline)) bool advance_lane_call(const void* ka, Lane& L, Frame* fr, bool hit, const Best& b,
-                                                            Query& q, Cnt& cnt, uint32_t job_rays) {
-    return advance_lane<COUNT, TEX>(kernel_params(ka), kernel_jobs(ka), ka, L, fr, hit, b, q, cnt, job_rays);
+                                                            uint64_t fanvis, Query& q, Cnt& cnt, uint32_t job_rays) {
+    return advance_lane<COUNT, TEX>(kernel_params(ka), kernel_jobs(ka), ka, L, fr, hit, b, fanvis, q, cnt, job_rays);
 }
 
 // Kernel variants (compile-time): bit 0 RT_V_CALL = state machine out of line (with RT_V_NOCOOP); bit 1 RT_V_NOPF = no node prefetch in the dynamic-fetch traversal; bit 2 RT_V_NOCOOP = no drain
@@ -861,9 +878,12 @@ __device__ __attribute__((noinline)) bool advance_lane_call(const void* ka, Lane
 
 template <bool COUNT, bool TEX, int V>
 __device__ __forceinline__ bool advance_v(const KParams& P, const JobSrc& J, const void* ka, Lane& L, Frame* fr,
-                                          bool hit, const Best& b, Query& q, Cnt& cnt, uint32_t job_rays) {
-    if constexpr ((V & RT_V_CALL) != 0) return advance_lane_call<COUNT, TEX>(ka, L, fr, hit, b, q, cnt, job_rays);
-    else return advance_lane<COUNT, TEX>(P, J, ka, L, fr, hit, b, q, cnt, job_rays);
+                                          bool hit, const Best& b, uint64_t fanvis, Query& q, Cnt& cnt,
+                                          uint32_t job_rays) {
+    if constexpr ((V & RT_V_CALL) != 0)
+        return advance_lane_call<COUNT, TEX>(ka, L, fr, hit, b, fanvis, q, cnt, job_rays);
+    else
+        return advance_lane<COUNT, TEX>(P, J, ka, L, fr, hit, b, fanvis, q, cnt, job_rays);
 }
 
 // ---- whole-traversal persistent kernel ------------------------------------------------------
@@ -926,7 +946,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_kernel(KParams P
         if (!busy) continue;
         if (COUNT && wave_leader()) cnt.wadv++;
         // ---- advance the state machine until the next query ----
-        need_trace = advance_v<COUNT, TEX, V>(P, J, ka, L, fr, hit, b, q, cnt, job_rays);
+        need_trace = advance_v<COUNT, TEX, V>(P, J, ka, L, fr, hit, b, 0ull, q, cnt, job_rays);
     }
     flush_counters<COUNT>(P, cnt);
     if (P.wave_trace && lane_id == 0) {  // wave trace: (start, end, jobs) per wave, 100 MHz clock
@@ -1420,6 +1440,54 @@ __device__ __forceinline__ void trav_finish(const DevScene& S, Trav& T) {
     }
 }
 
+// ---- spherical-light fans (dynamic-fetch kernel, all-opaque scenes, P.fan) -------------------
+// getSpherelights (src/shadow.cpp:145-215) traces the light's centre and then sl_m * sl_n samples
+// (sl_n spokes of sl_m rings) from one shading point, one cansee each.  Traced one after the other by
+// the lane that owns the pixel, a 64-sample light keeps that lane busy for 64 traversals while the
+// rest of the wave moves on.  Here the lane posts the light as a fan in its wave's LDS table and
+// every lane whose traversal slot is free takes samples of any posted fan: the samples of one shading
+// point run side by side (nearly the same nodes, so the wave stays coherent) and the pixel waits for
+// one traversal's time instead of 64.  A sample is the same cansee query (fan_sample_query restates
+// the loop's target arithmetic for sample s); the owner resumes with the visibility mask, and in an
+// opaque scene the loop's sums are counts of visible samples, so the result is bit-identical.
+#define FAN_SLOTS 16
+struct FanTable {
+    int owner[FAN_SLOTS];   // lane, -1 free
+    int next[FAN_SLOTS];    // next sample to hand out
+    int count[FAN_SLOTS];   // samples: centre + sl_m * sl_n (<= 64)
+    int done[FAN_SLOTS];    // samples finished
+    int traced[FAN_SLOTS];  // samples that needed a query (the owner's ray count)
+    int li[FAN_SLOTS];      // the spherical light
+    float hx[FAN_SLOTS], hy[FAN_SLOTS], hz[FAN_SLOTS];  // the shading point
+    unsigned long long vis[FAN_SLOTS];                  // bit s: sample s visible
+};
+
+// Sample s of a fan (0: the centre; s >= 1: the loop's sample ls = s - 1): the cansee query of
+// getSpherelights with the target the loop builds (its perp rotated once per finished spoke).
+// False when the target is within SHADOW_ERROR_OFFSET (visible without a query).
+__device__ __forceinline__ bool fan_sample_query(const KParams& P, v3 hp, int li, int s, Query& q, float& sdist) {
+    const rt_spherical_light sl = P.S.sl[li];
+    const v3 lp = ld3(sl.position);
+    v3 target = lp;
+    if (s > 0) {
+        const int m = P.sl_m, ls = s - 1, j = ls % m, k = ls / m;
+        v3 u0 = sphere_perp(hp, lp, sl.radius);
+        if (k > 0) {
+            const m3 rot = rodrigues(P.sl_sin, P.sl_1mcos, normalize(lp - hp));
+            for (int i = 0; i < k; ++i) u0 = mul(rot, u0);
+        }
+        target = lp + ((float)(m - j) / (float)m) * u0;
+    }
+    v3 d = target - hp;  // start_cansee
+    sdist = length(d);
+    d = normalize(d);
+    if (!(sdist > 0.0005f)) return false;
+    q.o = hp + 0.0005f * d;
+    q.d = d;
+    q.t = FLT_MAX;
+    return true;
+}
+
 template <bool COUNT, bool TEX, int V>
 __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParams P, JobSrc J) {
     // the drain lane groups run inline only: with the out-of-line state machine (RT_V_CALL) the variant
@@ -1429,12 +1497,18 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
     __shared__ int coop_pool[COOP_POOL];   // drain: node groups of the wave's last queries
     __shared__ int coop_q[CQ_N * COOP_Q];  // drain: those queries
     __shared__ int s_base, s_lim;
+    __shared__ FanTable ft;
     const int lane_id = threadIdx.x;
     int* stk = stack_lds + lane_id;
     const void* ka = (const void*)__builtin_amdgcn_kernarg_segment_ptr();  // this kernel's (P, J)
     const unsigned long long t_wave0 = P.wave_trace ? wall_clock64() : 0ull;
     unsigned int wave_jobs = 0;  // jobs this wave took (wave trace)
     const DevScene& S = P.S;
+    if (lane_id < FAN_SLOTS) ft.owner[lane_id] = -1;
+    __syncthreads();
+    int own_fan = -1;             // fan slot this lane's state machine waits for
+    bool fan_req = false;         // the state machine posted a fan, no free slot yet
+    int ray_fan = -1, ray_s = 0;  // the fan sample this lane's traversal slot traces
     Frame fr[RT_MAX_DEPTH];
     Lane L;
     L.job = -1;
@@ -1456,16 +1530,105 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
         if (P.wave_trace && t_exh) pa_drain++;
         bool start = false;
         Query q;
-        if (pending) {
+        bool qshadow = false;  // the new query's kind and cansee distance
+        float qsdist = 0.0f;
+        // fan samples that finished: into their fan's mask
+        if (pending && ray_fan >= 0) {
+            pending = false;
+            if (!T.found) atomicOr(&ft.vis[ray_fan], 1ull << ray_s);
+            atomicAdd(&ft.done[ray_fan], 1);
+            ray_fan = -1;
+        }
+        __syncthreads();
+        // the owners of complete fans resume with the mask
+        bool fan_done = false;
+        uint64_t fanvis = 0ull;
+        if (own_fan >= 0 && ft.done[own_fan] == ft.count[own_fan]) {
+            fanvis = ft.vis[own_fan];
+            job_rays += (uint32_t)ft.traced[own_fan];
+            ft.owner[own_fan] = -1;
+            own_fan = -1;
+            fan_done = true;
+        }
+        if (pending || fan_done) {
             pending = false;
             if (COUNT && wave_leader()) cnt.wadv++;
             q.o = T.o;
             q.d = T.d;
-            start = advance_v<COUNT, TEX, V>(P, J, ka, L, fr, T.found, T.best, q, cnt, job_rays);
+            start = advance_v<COUNT, TEX, V>(P, J, ka, L, fr, T.found, T.best, fanvis, q, cnt, job_rays);
+            if (start && L.ls == -2) {  // posted a fan
+                start = false;
+                fan_req = true;
+            }
+            qshadow = L.shadow;
+            qsdist = L.sdist;
+        }
+        __syncthreads();
+        if (P.fan) {
+            // free slots to the posted fans, in lane order
+            unsigned long long rq = __ballot(fan_req);
+            if (rq) {
+                uint64_t freeslots = __ballot(lane_id < FAN_SLOTS && ft.owner[lane_id] < 0);
+                while (rq && freeslots) {
+                    const int l = __ffsll((long long)rq) - 1, f = __ffsll((long long)freeslots) - 1;
+                    rq &= rq - 1ull;
+                    freeslots &= freeslots - 1ull;
+                    if (lane_id == l) {
+                        ft.owner[f] = l;
+                        ft.next[f] = 0;
+                        ft.count[f] = 1 + P.sl_m * P.sl_n;
+                        ft.done[f] = 0;
+                        ft.traced[f] = 0;
+                        ft.vis[f] = 0ull;
+                        ft.li[f] = L.li;
+                        ft.hx[f] = L.hp.x;
+                        ft.hy[f] = L.hp.y;
+                        ft.hz[f] = L.hp.z;
+                        own_fan = f;
+                        fan_req = false;
+                    }
+                }
+                __syncthreads();
+            }
+            // samples of the posted fans to every lane whose traversal slot is free, in slot order
+            const bool tfree = !tracing && !start;
+            const unsigned long long fl = __ballot(tfree);
+            uint64_t pend = __ballot(lane_id < FAN_SLOTS && ft.owner[lane_id] >= 0 && ft.next[lane_id] < ft.count[lane_id]);
+            if (fl && pend) {
+                const int nfree = __popcll(fl);
+                const int rank = __popcll(fl & ((1ull << lane_id) - 1ull));
+                int base = 0;
+                while (pend && base < nfree) {
+                    const int f = __ffsll((long long)pend) - 1;
+                    pend &= pend - 1ull;
+                    const int nx = ft.next[f];
+                    const int take = min(ft.count[f] - nx, nfree - base);
+                    if (tfree && rank >= base && rank < base + take) {
+                        ray_fan = f;
+                        ray_s = nx + (rank - base);
+                    }
+                    __syncthreads();
+                    if (lane_id == 0) ft.next[f] = nx + take;
+                    base += take;
+                }
+                if (tfree && ray_fan >= 0) {
+                    const v3 hp{ft.hx[ray_fan], ft.hy[ray_fan], ft.hz[ray_fan]};
+                    if (fan_sample_query(P, hp, ft.li[ray_fan], ray_s, q, qsdist)) {
+                        start = true;
+                        qshadow = true;
+                        atomicAdd(&ft.traced[ray_fan], 1);
+                    } else {  // visible without a query
+                        atomicOr(&ft.vis[ray_fan], 1ull << ray_s);
+                        atomicAdd(&ft.done[ray_fan], 1);
+                        ray_fan = -1;
+                    }
+                }
+                __syncthreads();
+            }
         }
         const unsigned long long tJ = COUNT ? (unsigned long long)clock64() : 0ull;
         if (COUNT) cnt.cyc_c += tJ - tA;  // state machine
-        const bool idle = (L.job == -1);
+        const bool idle = (L.job == -1) && !start && !tracing;
         const unsigned long long want = __ballot(idle);
         if (want) {
             const int nwant = __popcll(want);
@@ -1491,6 +1654,8 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
                 const int job_k = base + __popcll(want & ((1ull << lane_id) - 1ull));
                 if (job_k < lim) {
                     start = start_job(P, J, L, job_k, q);
+                    qshadow = false;
+                    qsdist = 0.0f;
                     job_rays = 0;
                 } else {
                     L.job = (J.xq && xtried < 8) ? -1 : -2;  // -2: no more work for this lane
@@ -1501,15 +1666,16 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
         if (COUNT) cnt.cyc_d += (unsigned long long)clock64() - tJ;  // job fetch and camera rays
         if (start) {
             cnt.rays++;
-            job_rays++;
-            trav_init_q(S, P.use_bvh != 0, q.o, q.d, q.t, L.shadow, L.sdist, T);
+            if (ray_fan < 0) job_rays++;  // a fan sample counts for its owner's job (ft.traced)
+            trav_init_q(S, P.use_bvh != 0, q.o, q.d, q.t, qshadow, qsdist, T);
             tracing = true;
         }
         if (P.wave_trace && !t_exh && __any(L.job == -2)) t_exh = wall_clock64();
         if (!__any(tracing)) {
-            if (!__any(L.job == -1 || pending)) break;  // every lane exhausted
+            if (!__any(L.job == -1 || pending || own_fan >= 0 || fan_req)) break;  // every lane exhausted
             continue;
         }
+        const bool fans = P.fan && __any(own_fan >= 0 || fan_req);  // lanes of exhausted waves take samples
         // ---- phase B: one node visit or one leaf record per lane and iteration ("if-if"), until
         // enough lanes wait for phase A ----
         unsigned long long tB = 0ull;
@@ -1532,7 +1698,8 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
                 pending = true;
             }
             if (!__any(tracing)) break;
-            if (__popcll(__ballot(pending || L.job == -1)) >= refill_at) break;
+            if (__popcll(__ballot(pending || L.job == -1 || (!tracing && (fans || own_fan >= 0 || fan_req)))) >= refill_at)
+                break;
             if (P.wave_trace && t_exh) {
                 it_drain++;
                 lanes_drain += (unsigned int)__popcll(__ballot(tracing));

@@ -61,6 +61,7 @@ struct rt_ctx {
     int opt_coop_max = 0;   // 0: the largest count the LDS pool allows
     int opt_refill = 0;     // 0: per render shape
     int opt_wave_trace = 0;
+    int opt_fan = 1;        // dynamic-fetch kernel: spherical-light samples as wave-shared fans
     int opt_variant = -1;   // -1: the shipped variant for the render shape (RT_DF_BATCH / _FRAME, RT_WT_DEFAULT)
     char last_kernel[64] = {0};
 };
@@ -526,6 +527,10 @@ extern "C" int rt_ctx_set_option(rt_ctx* c, int option, int value) {
         case RT_OPT_WAVE_TRACE:
             c->opt_wave_trace = value ? 1 : 0;
             return RT_OK;
+        case RT_OPT_FAN:
+            if (value < 0 || value > 1) break;
+            c->opt_fan = value;
+            return RT_OK;
         case RT_OPT_VARIANT:
             if (value < -1 || value > 255) break;
             c->opt_variant = value;
@@ -766,6 +771,9 @@ static void shape_options(const rt_ctx* c, KParams& K) {
     if (c->opt_coop >= 0) K.coop = c->opt_coop;
     if (c->opt_coop_max > 0) K.coop_max = std::min(K.coop_max, c->opt_coop_max);
     if (K.coop_max <= 0) K.coop = 0;
+    // spherical lights as wave-shared fans (rt_megakernel.hip FanTable): dynamic-fetch kernel, opaque
+    // scenes (every sample a plain any-hit query), at most 64 samples per light (one mask)
+    K.fan = (c->opt_fan && use_df(c) && K.S.all_opaque && K.S.nsl > 0 && 1 + K.sl_m * K.sl_n <= 64) ? 1 : 0;
 }
 
 static int launch_render(rt_ctx* c, KParams& K, hipStream_t st, int count_mode, rt_stats* stats) {

@@ -316,3 +316,38 @@ def _view_batch_checks(R, O, scene, ctx, prm, cfg, aa):
     ref, rays = O.Oracle(scene).render(prm, W, H, euler=R.turntable_eulers(5)[2])
     assert st1.rays == rays
     assert float(np.max(np.abs(img - ref))) <= TOL
+
+
+def test_sphere_light_fans_match_oracle(R, O, ctxs):
+    """Spherical-light samples traced as wave-shared fans (dynamic-fetch kernel, opaque scene) give
+    the per-lane loop's bits and ray counts, for frames and for rt_shade's explicit rays (whose
+    per-ray counts include the fan samples other lanes traced), and match the oracle."""
+    scene, ctx, prm, _, _ = ctxs("C4", (200, 80))
+    W, H = 64, 36
+    cam = R.camera_from_trackball(aspect=R.aspect_of(W, H))
+    out = {}
+    for fan in (1, 0):
+        with V.options(R, ctx, {R.OPT_KERNEL: R.KERNEL_DYNAMIC_FETCH, R.OPT_FAN: fan}):
+            out[fan] = ctx.render(cam, prm, W, H)
+    assert out[1][0].tobytes() == out[0][0].tobytes()
+    assert out[1][1].rays == out[0][1].rays
+    ref, rays = O.Oracle(scene).render(prm, W, H)
+    assert out[1][1].rays == rays
+    assert float(np.max(np.abs(out[1][0] - ref))) <= TOL
+    # rt_shade: 256 rays from one eye point towards random points around the model, level 0
+    rng = np.random.default_rng(5)
+    rays_in = np.zeros(256, R.RAY_DTYPE)
+    hits = rng.uniform(-0.4, 0.4, (len(rays_in), 3)).astype(np.float32)
+    rays_in["origin"] = np.float32([0.0, 0.2, -3.0])
+    dirs = hits - rays_in["origin"]
+    rays_in["direction"] = dirs / np.linalg.norm(dirs, axis=1, keepdims=True)
+    rays_in["t"] = np.float32(np.finfo(np.float32).max)
+    got = {}
+    for fan in (1, 0):
+        with V.options(R, ctx, {R.OPT_KERNEL: R.KERNEL_DYNAMIC_FETCH, R.OPT_FAN: fan}):
+            got[fan] = ctx.shade(rays_in, prm)
+    assert got[1][0].tobytes() == got[0][0].tobytes()
+    assert np.array_equal(got[1][1], got[0][1])
+    rgb_ref, cnt_ref = O.Oracle(scene).shade(rays_in, prm)
+    assert np.array_equal(got[1][1], cnt_ref)
+    assert float(np.max(np.abs(got[1][0] - rgb_ref))) <= TOL

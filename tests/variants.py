@@ -4,7 +4,8 @@ import contextlib
 
 
 def defaults(R):
-    return {R.OPT_KERNEL: R.KERNEL_AUTO, R.OPT_VARIANT: -1, R.OPT_COOP: -1, R.OPT_COOP_MAX: 0, R.OPT_REFILL: 0}
+    return {R.OPT_KERNEL: R.KERNEL_AUTO, R.OPT_VARIANT: -1, R.OPT_COOP: -1, R.OPT_COOP_MAX: 0, R.OPT_REFILL: 0,
+            R.OPT_FAN: 1}
 
 
 def kernel_classes(R):
@@ -21,6 +22,8 @@ def all_variants(R):
         {R.OPT_KERNEL: df, R.OPT_COOP_MAX: 1},                  # drain groups of 64 lanes only
         {R.OPT_KERNEL: df, R.OPT_COOP: 2, R.OPT_REFILL: 64},    # full-wave refill + straggler groups
         {R.OPT_KERNEL: df, R.OPT_REFILL: 8},
+        {R.OPT_KERNEL: df, R.OPT_FAN: 0},                       # spherical-light samples per lane
+        {R.OPT_KERNEL: df, R.OPT_VARIANT: R.DF_BATCH, R.OPT_FAN: 0},
     ]
     return out
 
