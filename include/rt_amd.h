@@ -327,6 +327,7 @@ int rt_debug_counters(rt_ctx* ctx, uint64_t* out, int n);
 #define RT_OPT_REFILL 4      /* dynamic-fetch kernel: waiting lanes that end a traversal phase (0: by shape) */
 #define RT_OPT_WAVE_TRACE 5  /* 1: record rt_debug_wave_trace data */
 #define RT_OPT_VARIANT 6     /* developer A/B: compiled kernel variant (rt_megakernel.hip RT_V_*), -1 default */
+#define RT_OPT_INTERLEAVE 8  /* job -> pixel order: -1 by render shape, 0 8x8 tiles per wave, 1 one pixel of each of 64 tiles per wave */
 #define RT_OPT_FAN 7         /* dynamic-fetch kernel, opaque scenes: spherical-light samples as wave-shared fans (1, default) or per lane (0) */
 #define RT_KERNEL_AUTO 0
 #define RT_KERNEL_WHOLE_TRAVERSAL 1
@@ -337,6 +338,9 @@ int rt_ctx_set_option(rt_ctx* ctx, int option, int value);
  * tracing lanes over them, 0, drain state-machine passes); timestamps of
  * the 100 MHz device clock.  Out holds 8 * max_waves words.  Returns the wave count. */
 int rt_debug_wave_trace(rt_ctx* ctx, uint64_t* out, int max_waves);
+/* ... and per job (pixel) of that launch: 3 words (start, end, queries of the job); out holds
+ * 3 * max_jobs words.  Returns the job count. */
+int rt_debug_job_trace(rt_ctx* ctx, uint64_t* out, int max_jobs);
 
 /* Introspection for tests / roofline accounting. */
 int rt_ctx_info(rt_ctx* ctx, int* num_nodes, int* num_tri_records, int* ref_bvh_nodes,

@@ -100,8 +100,10 @@ struct KParams {
     int refill;                 // dynamic-fetch kernel: waiting lanes that end a traversal phase
     int shade_level;            // rt_shade: recursion level of the explicit rays (getFinalColor's `level`)
     int fan;                    // dynamic-fetch kernel: spherical-light samples traced as wave-shared fans
+    int interleave;             // job -> pixel: a wave's 64 jobs are one pixel of each of 64 tiles
     uint32_t seed_lo, seed_hi;  // glossy sampling: Philox-4x32-10 key (rt_params.rng_seed)
     unsigned long long* wave_trace;  // developer wave trace (rt_ctx_set_option RT_OPT_WAVE_TRACE), or null
+    unsigned long long* job_trace;   // ... and per job: start, end (100 MHz clock), queries
     int coop;                        // dynamic-fetch kernel: lane-group traversal of the drain's queries
     int coop_max;                    // ... when at most this many queries are left in the wave
     int coop_reserve;                // ... free pool slots kept for depth-first steps

@@ -722,7 +722,14 @@ __device__ __forceinline__ void queue_camera(const KParams& P, Lane& L, Query& q
 // pixel's row in the band buffer.  False if outside the image.
 __device__ __forceinline__ bool job_pixel(const KParams& P, int gjob, uint32_t& rpix, int& out_row) {
     int view;
-    const int job = view_job(P, gjob, view);
+    int job = view_job(P, gjob, view);
+    if (P.interleave) {
+        // blocks of 64 tiles: the block's r-th job is pixel r / nb of its tile r % nb, so the 64
+        // jobs one wave takes lie in 64 tiles, and an expensive patch of the image is shared by
+        // many waves instead of held by one
+        const int nt = P.view_jobs >> 6, b = job >> 12, nb = min(64, nt - (b << 6)), r = job & 4095;
+        job = (((b << 6) + r % nb) << 6) + r / nb;
+    }
     const int tiles_x = (P.W + 7) / 8;
     const int tiles_y_band = (P.band_rows + 7) / 8;
     const int tile = job >> 6;
@@ -873,6 +880,7 @@ __device__ __attribute__((noinline)) bool advance_lane_call(const void* ka, Lane
 #define RT_V_W3 8
 #define RT_V_W4 16  // compiled for 4 waves per SIMD (128 VGPRs)
 #define RT_V_W5 128  // compiled for 5 waves per SIMD (~100 VGPRs)
+#define RT_V_FAN 256  // dynamic fetch: the spherical-light sample fans compiled in (P.fan)
 #define RT_V_WAVES(V) (((V) & RT_V_W5) ? 5 : ((V) & RT_V_W4) ? 4 : (((V) & RT_V_W3) ? 3 : 2))
 
 
@@ -1488,11 +1496,19 @@ __device__ __forceinline__ bool fan_sample_query(const KParams& P, v3 hp, int li
     return true;
 }
 
+// a sample of fan slot f finished: into the fan's mask, then its count (the owner reads the mask
+// once the count is complete)
+__device__ __forceinline__ void fan_record(FanTable& ft, int f, int s, bool vis) {
+    if (vis) atomicOr(&ft.vis[f], 1ull << s);
+    atomicAdd(&ft.done[f], 1);
+}
+
 template <bool COUNT, bool TEX, int V>
 __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParams P, JobSrc J) {
     // the drain lane groups run inline only: with the out-of-line state machine (RT_V_CALL) the variant
     // is compiled without them (an out-of-line drain call there lost values the kernel held across it)
-    constexpr bool PF = !(V & RT_V_NOPF), COOP = !(V & (RT_V_NOCOOP | RT_V_CALL));
+    constexpr bool PF = !(V & RT_V_NOPF), COOP = !(V & (RT_V_NOCOOP | RT_V_CALL)), FANS = (V & RT_V_FAN) != 0;
+    const bool fan_on = FANS && P.fan;  // (the host sets P.fan only for FANS variants)
     __shared__ int stack_lds[RT_STACK8 * RT_WAVE];
     __shared__ int coop_pool[COOP_POOL];   // drain: node groups of the wave's last queries
     __shared__ int coop_q[CQ_N * COOP_Q];  // drain: those queries
@@ -1504,8 +1520,13 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
     const unsigned long long t_wave0 = P.wave_trace ? wall_clock64() : 0ull;
     unsigned int wave_jobs = 0;  // jobs this wave took (wave trace)
     const DevScene& S = P.S;
-    if (lane_id < FAN_SLOTS) ft.owner[lane_id] = -1;
-    __syncthreads();
+    if (FANS) {
+        if (lane_id < FAN_SLOTS) ft.owner[lane_id] = -1;
+        __syncthreads();
+    }
+    __shared__ int fan_queue[RT_WAVE];  // lanes waiting for a fan slot, oldest first
+    int fq_head = 0, fq_tail = 0;       // (wave-uniform)
+    int fq_in = 0;                      // this lane is in the queue
     int own_fan = -1;             // fan slot this lane's state machine waits for
     bool fan_req = false;         // the state machine posted a fan, no free slot yet
     int ray_fan = -1, ray_s = 0;  // the fan sample this lane's traversal slot traces
@@ -1533,17 +1554,16 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
         bool qshadow = false;  // the new query's kind and cansee distance
         float qsdist = 0.0f;
         // fan samples that finished: into their fan's mask
-        if (pending && ray_fan >= 0) {
+        if (FANS && pending && ray_fan >= 0) {
             pending = false;
-            if (!T.found) atomicOr(&ft.vis[ray_fan], 1ull << ray_s);
-            atomicAdd(&ft.done[ray_fan], 1);
+            fan_record(ft, ray_fan, ray_s, !T.found);
             ray_fan = -1;
         }
-        __syncthreads();
+        if (FANS) __syncthreads();
         // the owners of complete fans resume with the mask
         bool fan_done = false;
         uint64_t fanvis = 0ull;
-        if (own_fan >= 0 && ft.done[own_fan] == ft.count[own_fan]) {
+        if (FANS && own_fan >= 0 && ft.done[own_fan] == ft.count[own_fan]) {
             fanvis = ft.vis[own_fan];
             job_rays += (uint32_t)ft.traced[own_fan];
             ft.owner[own_fan] = -1;
@@ -1555,25 +1575,41 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
             if (COUNT && wave_leader()) cnt.wadv++;
             q.o = T.o;
             q.d = T.d;
+            const int jb = L.job;
             start = advance_v<COUNT, TEX, V>(P, J, ka, L, fr, T.found, T.best, fanvis, q, cnt, job_rays);
-            if (start && L.ls == -2) {  // posted a fan
+            if (P.job_trace && L.job == -1) {
+                P.job_trace[3 * jb + 1] = wall_clock64();
+                P.job_trace[3 * jb + 2] = job_rays;
+            }
+            if (FANS && start && L.ls == -2) {  // posted a fan
                 start = false;
                 fan_req = true;
             }
             qshadow = L.shadow;
             qsdist = L.sdist;
         }
-        __syncthreads();
-        if (P.fan) {
-            // free slots to the posted fans, in lane order
-            unsigned long long rq = __ballot(fan_req);
-            if (rq) {
+        if (fan_on) {
+            __syncthreads();
+            // the fans posted in this pass join the wave's queue; free slots go to the oldest (in
+            // lane order, a busy wave's high lanes could wait for ever)
+            const bool new_req = fan_req && fq_in == 0;
+            const unsigned long long nr = __ballot(new_req);
+            if (nr) {
+                if (new_req) {
+                    fan_queue[(fq_tail + __popcll(nr & ((1ull << lane_id) - 1ull))) & (RT_WAVE - 1)] = lane_id;
+                    fq_in = 1;
+                }
+                fq_tail += __popcll(nr);
+                __syncthreads();
+            }
+            if (fq_head != fq_tail) {
                 uint64_t freeslots = __ballot(lane_id < FAN_SLOTS && ft.owner[lane_id] < 0);
-                while (rq && freeslots) {
-                    const int l = __ffsll((long long)rq) - 1, f = __ffsll((long long)freeslots) - 1;
-                    rq &= rq - 1ull;
+                while (fq_head != fq_tail && freeslots) {
+                    const int l = fan_queue[fq_head & (RT_WAVE - 1)], f = __ffsll((long long)freeslots) - 1;
+                    ++fq_head;
                     freeslots &= freeslots - 1ull;
                     if (lane_id == l) {
+                        fq_in = 0;
                         ft.owner[f] = l;
                         ft.next[f] = 0;
                         ft.count[f] = 1 + P.sl_m * P.sl_n;
@@ -1611,24 +1647,29 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
                     if (lane_id == 0) ft.next[f] = nx + take;
                     base += take;
                 }
-                if (tfree && ray_fan >= 0) {
-                    const v3 hp{ft.hx[ray_fan], ft.hy[ray_fan], ft.hz[ray_fan]};
-                    if (fan_sample_query(P, hp, ft.li[ray_fan], ray_s, q, qsdist)) {
-                        start = true;
-                        qshadow = true;
-                        atomicAdd(&ft.traced[ray_fan], 1);
-                    } else {  // visible without a query
-                        atomicOr(&ft.vis[ray_fan], 1ull << ray_s);
-                        atomicAdd(&ft.done[ray_fan], 1);
-                        ray_fan = -1;
-                    }
-                }
                 __syncthreads();
             }
+            if (tfree && ray_fan >= 0) {
+                const v3 hp{ft.hx[ray_fan], ft.hy[ray_fan], ft.hz[ray_fan]};
+                if (fan_sample_query(P, hp, ft.li[ray_fan], ray_s, q, qsdist)) {
+                    start = true;
+                    qshadow = true;
+                    atomicAdd(&ft.traced[ray_fan], 1);
+                } else {  // visible without a query
+                    fan_record(ft, ray_fan, ray_s, true);
+                    ray_fan = -1;
+                }
+            }
+            __syncthreads();
         }
         const unsigned long long tJ = COUNT ? (unsigned long long)clock64() : 0ull;
         if (COUNT) cnt.cyc_c += tJ - tA;  // state machine
-        const bool idle = (L.job == -1) && !start && !tracing;
+        // a wave whose pixels wait on FAN_SLOTS fans takes no new pixels: its free lanes trace fan
+        // samples, so a cluster of expensive pixels is spread over the wave's lanes instead of each
+        // lane carrying one pixel's samples alone (and a wave holds few expensive pixels when the
+        // job queue runs dry)
+        const bool fan_full = fan_on && __popcll(__ballot(own_fan >= 0 || fan_req)) >= FAN_SLOTS;
+        const bool idle = (L.job == -1) && !start && !tracing && !fan_full;
         const unsigned long long want = __ballot(idle);
         if (want) {
             const int nwant = __popcll(want);
@@ -1653,6 +1694,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
             if (idle) {
                 const int job_k = base + __popcll(want & ((1ull << lane_id) - 1ull));
                 if (job_k < lim) {
+                    if (P.job_trace) P.job_trace[3 * job_k] = wall_clock64();
                     start = start_job(P, J, L, job_k, q);
                     qshadow = false;
                     qsdist = 0.0f;
@@ -1671,11 +1713,12 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
             tracing = true;
         }
         if (P.wave_trace && !t_exh && __any(L.job == -2)) t_exh = wall_clock64();
+        // device-wide fans with samples not yet handed out (waves out of pixels stay to take them)
         if (!__any(tracing)) {
             if (!__any(L.job == -1 || pending || own_fan >= 0 || fan_req)) break;  // every lane exhausted
             continue;
         }
-        const bool fans = P.fan && __any(own_fan >= 0 || fan_req);  // lanes of exhausted waves take samples
+        const bool fans = fan_on && __any(own_fan >= 0 || fan_req);  // lanes of exhausted waves take samples
         // ---- phase B: one node visit or one leaf record per lane and iteration ("if-if"), until
         // enough lanes wait for phase A ----
         unsigned long long tB = 0ull;

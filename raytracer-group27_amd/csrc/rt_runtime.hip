@@ -45,13 +45,14 @@ struct rt_ctx {
     int bvh8_depth = 0;
     bool df_ok = true;  // the BVH8 fits the dynamic-fetch kernel's LDS stack
     bool glossy_material = false;  // opaque, ks > 0, shininess != 0 (glossy_ray_count > 1 draws lobes)
-    int persistent_blocks[512] = {0};  // resident 64-lane blocks per (kernel class, variant)
+    int persistent_blocks[1024] = {0};  // resident 64-lane blocks per (kernel class, variant)
     // lights (re-uploadable: rt_update_lights)
     void* d_lights[4] = {nullptr, nullptr, nullptr, nullptr};
     // developer wave trace (RT_OPT_WAVE_TRACE)
     float* d_wave_trace = nullptr;
     size_t wave_trace_bytes = 0;
     int wave_trace_n = 0;
+    int job_trace_n = 0;
     // view batch (rt_render_views_device): per-view cameras, 12 floats each
     float* d_views = nullptr;
     size_t views_bytes = 0;
@@ -62,6 +63,7 @@ struct rt_ctx {
     int opt_refill = 0;     // 0: per render shape
     int opt_wave_trace = 0;
     int opt_fan = 1;        // dynamic-fetch kernel: spherical-light samples as wave-shared fans
+    int opt_interleave = -1;  // job -> pixel interleave: -1 by render shape, 0 off, 1 on
     int opt_variant = -1;   // -1: the shipped variant for the render shape (RT_DF_BATCH / _FRAME, RT_WT_DEFAULT)
     char last_kernel[64] = {0};
 };
@@ -527,12 +529,16 @@ extern "C" int rt_ctx_set_option(rt_ctx* c, int option, int value) {
         case RT_OPT_WAVE_TRACE:
             c->opt_wave_trace = value ? 1 : 0;
             return RT_OK;
+        case RT_OPT_INTERLEAVE:
+            if (value < -1 || value > 1) break;
+            c->opt_interleave = value;
+            return RT_OK;
         case RT_OPT_FAN:
             if (value < 0 || value > 1) break;
             c->opt_fan = value;
             return RT_OK;
         case RT_OPT_VARIANT:
-            if (value < -1 || value > 255) break;
+            if (value < -1 || value > 511) break;
             c->opt_variant = value;
             return RT_OK;
         default:
@@ -566,10 +572,12 @@ static bool use_df(const rt_ctx* c) {
 #define RT_DF_ALT2 (RT_V_CALL | RT_V_NOPF | RT_V_NOCOOP | RT_V_W5)
 #define RT_WT_ALT1 (RT_V_CALL | RT_V_W3)
 
-static int variant_of(const rt_ctx* c, bool df, int n_views) {
-    if (c->opt_variant >= 0) return c->opt_variant;
-    if (!df) return RT_WT_DEFAULT;
-    return n_views > 1 ? RT_DF_BATCH : RT_DF_FRAME;
+// by render shape: view batches and sample-fan renders run the lean 4-wave variant (C4 single frame
+// with fans: 27.1 vs 30.3 ms), other single frames the 2-wave variant with the drain lane groups
+static int variant_of(const rt_ctx* c, bool df, const KParams& K) {
+    if (!df) return c->opt_variant >= 0 ? c->opt_variant : RT_WT_DEFAULT;
+    const int v = c->opt_variant >= 0 ? c->opt_variant : ((K.n_views > 1 || K.fan) ? RT_DF_BATCH : RT_DF_FRAME);
+    return K.fan ? (v | RT_V_FAN) : v;  // shape_options keeps K.fan to variants compiled with fans
 }
 
 template <bool DF, bool COUNT, bool TEX, int V>
@@ -584,6 +592,7 @@ static void launch_v(int grid, hipStream_t st, const KParams& K, const JobSrc& J
 template <bool COUNT, bool TEX>
 static bool launch_shipped(bool df, int v, int grid, hipStream_t st, const KParams& K, const JobSrc& J) {
     if (df && v == RT_DF_BATCH) launch_v<true, COUNT, TEX, RT_DF_BATCH>(grid, st, K, J);
+    else if (df && v == (RT_DF_BATCH | RT_V_FAN)) launch_v<true, COUNT, TEX, RT_DF_BATCH | RT_V_FAN>(grid, st, K, J);
     else if (df && v == RT_DF_FRAME) launch_v<true, COUNT, TEX, RT_DF_FRAME>(grid, st, K, J);
     else if (!df && v == RT_WT_DEFAULT) launch_v<false, COUNT, TEX, RT_WT_DEFAULT>(grid, st, K, J);
     else return false;
@@ -594,7 +603,7 @@ template <bool COUNT>
 static int launch_persistent(int grid, hipStream_t st, const KParams& K, const JobSrc& J, rt_ctx* c) {
     const bool df = use_df(c);
     const bool tex = COUNT || K.S.tex_on;  // counting builds keep the texture code (one instance each)
-    const int v = variant_of(c, df, K.n_views);
+    const int v = variant_of(c, df, K);
     bool ok = tex ? launch_shipped<COUNT, true>(df, v, grid, st, K, J) : launch_shipped<COUNT, false>(df, v, grid, st, K, J);
     if (!ok && !COUNT && !tex) {
         ok = true;
@@ -623,16 +632,17 @@ static int occupancy_of(int* per_cu) {
 }
 
 // resident 64-lane blocks of the kernel (the persistent grid)
-static int persistent_grid(rt_ctx* c, int n_views) {
+static int persistent_grid(rt_ctx* c, const KParams& K) {
     const bool df = use_df(c);
-    const int v = variant_of(c, df, n_views);
-    const int key = (df ? 256 : 0) + (v & 255);
+    const int v = variant_of(c, df, K);
+    const int key = (df ? 512 : 0) + (v & 511);
     if (c->persistent_blocks[key] > 0) return c->persistent_blocks[key];
     int cus = 0, per_cu = 0;
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
     int e = 1;
     if (df) {
         if (v == RT_DF_BATCH) e = occupancy_of<true, RT_DF_BATCH>(&per_cu);
+        else if (v == (RT_DF_BATCH | RT_V_FAN)) e = occupancy_of<true, RT_DF_BATCH | RT_V_FAN>(&per_cu);
         else if (v == RT_DF_FRAME) e = occupancy_of<true, RT_DF_FRAME>(&per_cu);
         else if (v == RT_DF_ALT1) e = occupancy_of<true, RT_DF_ALT1>(&per_cu);
         else e = occupancy_of<true, RT_DF_ALT2>(&per_cu);
@@ -774,6 +784,10 @@ static void shape_options(const rt_ctx* c, KParams& K) {
     // spherical lights as wave-shared fans (rt_megakernel.hip FanTable): dynamic-fetch kernel, opaque
     // scenes (every sample a plain any-hit query), at most 64 samples per light (one mask)
     K.fan = (c->opt_fan && use_df(c) && K.S.all_opaque && K.S.nsl > 0 && 1 + K.sl_m * K.sl_n <= 64) ? 1 : 0;
+    if (c->opt_variant >= 0 && c->opt_variant != RT_DF_BATCH) K.fan = 0;  // fans are compiled into that variant only
+    // single frames with fans: a wave's jobs spread over 64 tiles (C4 52.9 -> 31.4 ms; the tile order
+    // keeps its coherence elsewhere: C3 2.18 vs 2.41 ms, C2 0.77 vs 0.98 ms)
+    K.interleave = c->opt_interleave >= 0 ? c->opt_interleave : (K.fan && K.n_views <= 1 ? 1 : 0);
 }
 
 static int launch_render(rt_ctx* c, KParams& K, hipStream_t st, int count_mode, rt_stats* stats) {
@@ -791,12 +805,16 @@ static int launch_render(rt_ctx* c, KParams& K, hipStream_t st, int count_mode, 
         K.view_jobs = J.view_jobs;
         J.counter = reinterpret_cast<int*>(c->d_stats + 7);
         J.xq = use_df(c) ? reinterpret_cast<int*>(c->d_stats + 16) : nullptr;
-        const int grid = (int)std::min<long long>(blocks * J.n_views, persistent_grid(c, K.n_views));
+        const int grid = (int)std::min<long long>(blocks * J.n_views, persistent_grid(c, K));
         if (c->opt_wave_trace) {
-            const int rc = ensure(c, &c->d_wave_trace, &c->wave_trace_bytes, (size_t)grid * 8 * 8);
+            const int rc = ensure(c, &c->d_wave_trace, &c->wave_trace_bytes,
+                                  (size_t)grid * 8 * 8 + (size_t)J.njobs * 3 * 8);
             if (rc != RT_OK) return rc;
             K.wave_trace = reinterpret_cast<unsigned long long*>(c->d_wave_trace);
+            K.job_trace = K.wave_trace + (size_t)grid * 8;
+            HIP_TRY(hipMemsetAsync(K.job_trace, 0, (size_t)J.njobs * 3 * 8, st));
             c->wave_trace_n = grid;
+            c->job_trace_n = J.njobs;
         }
         HIP_TRY(hipEventRecord(c->ev0, st));
         const int lrc = count_mode ? launch_persistent<true>(grid, st, K, J, c) : launch_persistent<false>(grid, st, K, J, c);
@@ -1044,8 +1062,10 @@ extern "C" int rt_shade(rt_ctx* c, const rt_ray* rays, int n, const rt_params* p
         J.view_jobs = n;
         J.counter = reinterpret_cast<int*>(c->d_stats + 7);
         J.xq = use_df(c) ? reinterpret_cast<int*>(c->d_stats + 16) : nullptr;
-        const int grid = std::min((n + 63) / 64, persistent_grid(c, 1));
-        if (launch_persistent<false>(grid, c->stream, K, J, c) != RT_OK) e = hipErrorInvalidValue;
+        const int grid = std::min((n + 63) / 64, persistent_grid(c, K));
+        const int lrc = g_count_mode ? launch_persistent<true>(grid, c->stream, K, J, c)
+                                     : launch_persistent<false>(grid, c->stream, K, J, c);
+        if (lrc != RT_OK) e = hipErrorInvalidValue;
         else e = hipGetLastError();
     }
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
@@ -1112,6 +1132,15 @@ extern "C" int rt_ctx_info(rt_ctx* c, int* num_nodes, int* num_tri_records, int*
     if (ref_bvh_nodes) *ref_bvh_nodes = c->ref_nodes;
     if (ref_bvh_levels) *ref_bvh_levels = c->ref_levels;
     return RT_OK;
+}
+
+extern "C" int rt_debug_job_trace(rt_ctx* c, uint64_t* out, int max_jobs) {
+    if (!c || !out || max_jobs <= 0) return RT_ERR_INVALID;
+    const int n = std::min(max_jobs, c->job_trace_n);
+    if (n > 0)
+        HIP_TRY(hipMemcpy(out, reinterpret_cast<unsigned long long*>(c->d_wave_trace) + (size_t)c->wave_trace_n * 8,
+                          (size_t)n * 3 * 8, hipMemcpyDeviceToHost));
+    return n;
 }
 
 extern "C" int rt_debug_wave_trace(rt_ctx* c, uint64_t* out, int max_waves) {

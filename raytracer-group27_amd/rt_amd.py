@@ -128,12 +128,13 @@ EXPORTS = [
     "rt_destroy", "rt_render", "rt_render_device", "rt_render_views_device", "rt_render_views", "rt_unpermute_bands_device", "rt_intersect", "rt_shade",
     "rt_set_counting", "rt_debug_counters", "rt_ctx_info", "rt_selftest_math",
     "rt_postprocess_device", "rt_bitmap_device", "rt_postprocess", "rt_bitmap", "rt_encode_bmp", "rt_write_bmp",
-    "rt_philox4x32_10", "rt_debug_wave_trace", "rt_decode_png", "rt_ctx_set_option", "rt_texture_sample",
+    "rt_philox4x32_10", "rt_debug_wave_trace", "rt_debug_job_trace", "rt_decode_png", "rt_ctx_set_option", "rt_texture_sample",
     "rt_update_lights", "rt_update_materials", "rt_unpermute_views_device", "rt_scene_mesh_count", "rt_scene_mesh_get",
 ]
 
 # rt_ctx_set_option (include/rt_amd.h): test / developer hooks; defaults are the shipped path
-OPT_KERNEL, OPT_COOP, OPT_COOP_MAX, OPT_REFILL, OPT_WAVE_TRACE, OPT_VARIANT, OPT_FAN = 1, 2, 3, 4, 5, 6, 7
+OPT_KERNEL, OPT_COOP, OPT_COOP_MAX, OPT_REFILL, OPT_WAVE_TRACE, OPT_VARIANT, OPT_FAN, OPT_INTERLEAVE = \
+    1, 2, 3, 4, 5, 6, 7, 8
 KERNEL_AUTO, KERNEL_WHOLE_TRAVERSAL, KERNEL_DYNAMIC_FETCH = 0, 1, 2
 # compiled kernel variants (rt_megakernel.hip RT_V_*, rt_runtime.hip RT_DF_* / RT_WT_*)
 V_CALL, V_NOPF, V_NOCOOP, V_W3, V_W4, V_W5 = 1, 2, 4, 8, 16, 128
@@ -261,6 +262,7 @@ def lib():
             "rt_decode_png": ([P(C.c_uint8), C.c_long, P(C.c_int), P(C.c_int), P(C.c_int), P(C.c_uint8), C.c_long],
                               C.c_int),
             "rt_debug_wave_trace": ([vp, P(C.c_uint64), C.c_int], C.c_int),
+            "rt_debug_job_trace": ([vp, P(C.c_uint64), C.c_int], C.c_int),
             "rt_ctx_set_option": ([vp, C.c_int, C.c_int], C.c_int),
             "rt_texture_sample": ([vp, C.c_int, C.c_int, P(C.c_float), P(rt_params), P(C.c_float)], C.c_int),
             "rt_update_lights": ([vp, P(rt_scene_desc)], C.c_int),

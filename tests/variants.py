@@ -5,7 +5,7 @@ import contextlib
 
 def defaults(R):
     return {R.OPT_KERNEL: R.KERNEL_AUTO, R.OPT_VARIANT: -1, R.OPT_COOP: -1, R.OPT_COOP_MAX: 0, R.OPT_REFILL: 0,
-            R.OPT_FAN: 1}
+            R.OPT_FAN: 1, R.OPT_INTERLEAVE: -1}
 
 
 def kernel_classes(R):
@@ -24,6 +24,9 @@ def all_variants(R):
         {R.OPT_KERNEL: df, R.OPT_REFILL: 8},
         {R.OPT_KERNEL: df, R.OPT_FAN: 0},                       # spherical-light samples per lane
         {R.OPT_KERNEL: df, R.OPT_VARIANT: R.DF_BATCH, R.OPT_FAN: 0},
+        {R.OPT_KERNEL: df, R.OPT_INTERLEAVE: 1, R.OPT_FAN: 0},  # a wave's pixels spread over 64 tiles
+        {R.OPT_KERNEL: df, R.OPT_INTERLEAVE: 0},
+        {R.OPT_KERNEL: wt, R.OPT_INTERLEAVE: 1},
     ]
     return out
 
