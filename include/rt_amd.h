@@ -327,6 +327,7 @@ int rt_debug_counters(rt_ctx* ctx, uint64_t* out, int n);
 #define RT_OPT_REFILL 4      /* dynamic-fetch kernel: waiting lanes that end a traversal phase (0: by shape) */
 #define RT_OPT_WAVE_TRACE 5  /* 1: record rt_debug_wave_trace data */
 #define RT_OPT_VARIANT 6     /* developer A/B: compiled kernel variant (rt_megakernel.hip RT_V_*), -1 default */
+#define RT_OPT_FAN_CAP 9     /* fan renders: pixels a wave may have waiting on fans before it takes no new ones (0: default 16) */
 #define RT_OPT_INTERLEAVE 8  /* job -> pixel order: -1 by render shape, 0 8x8 tiles per wave, 1 one pixel of each of 64 tiles per wave */
 #define RT_OPT_FAN 7         /* dynamic-fetch kernel, opaque scenes: spherical-light samples as wave-shared fans (1, default) or per lane (0) */
 #define RT_KERNEL_AUTO 0

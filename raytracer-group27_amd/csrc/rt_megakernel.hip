@@ -1664,11 +1664,11 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
         }
         const unsigned long long tJ = COUNT ? (unsigned long long)clock64() : 0ull;
         if (COUNT) cnt.cyc_c += tJ - tA;  // state machine
-        // a wave whose pixels wait on FAN_SLOTS fans takes no new pixels: its free lanes trace fan
+        // a wave whose pixels wait on P.fan_cap fans takes no new pixels: its free lanes trace fan
         // samples, so a cluster of expensive pixels is spread over the wave's lanes instead of each
         // lane carrying one pixel's samples alone (and a wave holds few expensive pixels when the
         // job queue runs dry)
-        const bool fan_full = fan_on && __popcll(__ballot(own_fan >= 0 || fan_req)) >= FAN_SLOTS;
+        const bool fan_full = fan_on && __popcll(__ballot(own_fan >= 0 || fan_req)) >= P.fan_cap;
         const bool idle = (L.job == -1) && !start && !tracing && !fan_full;
         const unsigned long long want = __ballot(idle);
         if (want) {

@@ -64,6 +64,7 @@ struct rt_ctx {
     int opt_wave_trace = 0;
     int opt_fan = 1;        // dynamic-fetch kernel: spherical-light samples as wave-shared fans
     int opt_interleave = -1;  // job -> pixel interleave: -1 by render shape, 0 off, 1 on
+    int opt_fan_cap = 0;      // pixels a wave may have waiting on fans before it stops taking new ones (0: default)
     int opt_variant = -1;   // -1: the shipped variant for the render shape (RT_DF_BATCH / _FRAME, RT_WT_DEFAULT)
     char last_kernel[64] = {0};
 };
@@ -529,6 +530,10 @@ extern "C" int rt_ctx_set_option(rt_ctx* c, int option, int value) {
         case RT_OPT_WAVE_TRACE:
             c->opt_wave_trace = value ? 1 : 0;
             return RT_OK;
+        case RT_OPT_FAN_CAP:
+            if (value < 0 || value > 64) break;
+            c->opt_fan_cap = value;
+            return RT_OK;
         case RT_OPT_INTERLEAVE:
             if (value < -1 || value > 1) break;
             c->opt_interleave = value;
@@ -785,6 +790,7 @@ static void shape_options(const rt_ctx* c, KParams& K) {
     // scenes (every sample a plain any-hit query), at most 64 samples per light (one mask)
     K.fan = (c->opt_fan && use_df(c) && K.S.all_opaque && K.S.nsl > 0 && 1 + K.sl_m * K.sl_n <= 64) ? 1 : 0;
     if (c->opt_variant >= 0 && c->opt_variant != RT_DF_BATCH) K.fan = 0;  // fans are compiled into that variant only
+    K.fan_cap = c->opt_fan_cap > 0 ? c->opt_fan_cap : 16;
     // single frames with fans: a wave's jobs spread over 64 tiles (C4 52.9 -> 31.4 ms; the tile order
     // keeps its coherence elsewhere: C3 2.18 vs 2.41 ms, C2 0.77 vs 0.98 ms)
     K.interleave = c->opt_interleave >= 0 ? c->opt_interleave : (K.fan && K.n_views <= 1 ? 1 : 0);
