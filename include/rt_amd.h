@@ -342,6 +342,9 @@ int rt_debug_wave_trace(rt_ctx* ctx, uint64_t* out, int max_waves);
 /* ... and per job (pixel) of that launch: 3 words (start, end, queries of the job); out holds
  * 3 * max_jobs words.  Returns the job count. */
 int rt_debug_job_trace(rt_ctx* ctx, uint64_t* out, int max_jobs);
+/* rt_create's phase clock, cumulative ms (device, reference BVH, BVH2/BVH8, records, materials and
+ * textures, uploads, total): up to n doubles. */
+int rt_debug_create_ms(rt_ctx* ctx, double* out, int n);
 
 /* Introspection for tests / roofline accounting. */
 int rt_ctx_info(rt_ctx* ctx, int* num_nodes, int* num_tri_records, int* ref_bvh_nodes,

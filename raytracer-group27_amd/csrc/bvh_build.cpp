@@ -7,9 +7,38 @@
 #include <cstring>
 #include <queue>
 #include <stdexcept>
+#include <string>
+#include <array>
+#include <atomic>
+#include <thread>
 #include <utility>
 
 namespace rt {
+
+namespace {
+// run f(i) for i in [0, n) on up to `threads` host threads
+template <typename F>
+void parallel_for(int n, int threads, F&& f) {
+    threads = std::max(1, std::min(threads, n));
+    if (threads == 1) {
+        for (int i = 0; i < n; ++i) f(i);
+        return;
+    }
+    std::atomic<int> next{0};
+    std::vector<std::thread> pool;
+    for (int t = 0; t < threads; ++t)
+        pool.emplace_back([&] {
+            for (int i = next++; i < n; i = next++) f(i);
+        });
+    for (std::thread& th : pool) th.join();
+}
+
+int host_threads() {
+    const unsigned hc = std::thread::hardware_concurrency();
+    return (int)std::max(1u, std::min(hc == 0 ? 1u : hc, 16u));
+}
+
+}  // namespace
 
 // ---------------------------------------------------------------------------------------------
 // Reference BVH: constructBVH / createNodeAndUpdateStats / createNodeFromObjects /
@@ -59,19 +88,90 @@ struct RefBuild {
         return attr == 0 ? s[0] : (attr == 1 ? s[1] : s[2]);
     }
 
-    int create_node(std::vector<int>&& objs, std::vector<uint8_t>&& is_tri, int level) {
+    int create_node(std::vector<int>&& objs, std::vector<uint8_t>&& is_tri, int level, const v3& lo, const v3& hi) {
         RefNode n;
         n.is_leaf = (objs.size() <= 1 || level >= max_level);
-        aabb(objs, is_tri, n.lower, n.upper);
+        n.lower = lo;
+        n.upper = hi;
         bvh.nodes.push_back(std::move(n));
         node_objs.push_back(std::move(objs));
         node_is_tri.push_back(std::move(is_tri));
         return (int)bvh.nodes.size() - 1;
     }
 
+    // createAabbFromObjects over a node's objects (min / max: any split of the loop gives the same box)
+    void aabb_par(const std::vector<int>& objs, const std::vector<uint8_t>& is_tri, v3& lo, v3& hi, int nth) const {
+        const int n = (int)objs.size(), ch = 1 << 15, nch = (n + ch - 1) / ch;
+        if (nch <= 1) {
+            aabb(objs, is_tri, lo, hi);
+            return;
+        }
+        std::vector<v3> clo(nch), chi(nch);
+        parallel_for(nch, nth, [&](int c) {
+            const int b = c * ch, e = std::min(n, b + ch);
+            std::vector<int> o(objs.begin() + b, objs.begin() + e);
+            std::vector<uint8_t> t(is_tri.begin() + b, is_tri.begin() + e);
+            aabb(o, t, clo[c], chi[c]);
+        });
+        lo = splat(FLT_MAX);
+        hi = splat(-FLT_MAX);
+        for (int c = 0; c < nch; ++c) {
+            lo = gmin(lo, clo[c]);
+            hi = gmax(hi, chi[c]);
+        }
+    }
+
+    // sortObjects' std::sort of (attribute, position) pairs as a stable LSD radix sort of the
+    // attribute (positions start in order, so equal attributes keep it, as the pair order does;
+    // -0 and +0 compare equal there and share a key here)
+    static void sort_order(const std::vector<float>& key, std::vector<int>& order, int nth) {
+        const int n = (int)key.size();
+        std::vector<uint32_t> k(n), k2(n);
+        std::vector<int> o2(n);
+        order.resize(n);
+        const int ch = 1 << 15, nch = std::max(1, (n + ch - 1) / ch);
+        parallel_for(nch, nth, [&](int c) {
+            for (int i = c * ch; i < std::min(n, (c + 1) * ch); ++i) {
+                const float f = key[i] == 0.0f ? 0.0f : key[i];
+                uint32_t u;
+                std::memcpy(&u, &f, 4);
+                k[i] = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+                order[i] = i;
+            }
+        });
+        // stable passes: per-chunk digit counts, digit-major offsets, then each chunk scatters its
+        // elements in order
+        std::vector<std::array<int, 256>> cnt(nch);
+        for (int shift = 0; shift < 32; shift += 8) {
+            parallel_for(nch, nth, [&](int c) {
+                cnt[c].fill(0);
+                for (int i = c * ch; i < std::min(n, (c + 1) * ch); ++i) cnt[c][(k[i] >> shift) & 255u]++;
+            });
+            int run = 0;
+            for (int d = 0; d < 256; ++d)
+                for (int c = 0; c < nch; ++c) {
+                    const int v = cnt[c][d];
+                    cnt[c][d] = run;
+                    run += v;
+                }
+            parallel_for(nch, nth, [&](int c) {
+                for (int i = c * ch; i < std::min(n, (c + 1) * ch); ++i) {
+                    const int d = cnt[c][(k[i] >> shift) & 255u]++;
+                    k2[d] = k[i];
+                    o2[d] = order[i];
+                }
+            });
+            k.swap(k2);
+            order.swap(o2);
+        }
+    }
+
     void build() {
+        const int nth = host_threads();
         std::vector<int> objs;
         std::vector<uint8_t> is_tri;
+        objs.reserve(ntri + nsph);
+        is_tri.reserve(ntri + nsph);
         for (int i = 0; i < ntri; ++i) {
             objs.push_back(i);
             is_tri.push_back(1);
@@ -81,47 +181,77 @@ struct RefBuild {
             is_tri.push_back(0);
         }
         bvh.max_level_achieved = objs.empty() ? -1 : 0;
-        if (!objs.empty()) bvh.max_level_achieved = 0;
-        std::queue<std::pair<int, int>> q;
-        create_node(std::move(objs), std::move(is_tri), 0);
-        q.push({0, 0});
-        while (!q.empty()) {
-            const int ni = q.front().first;
-            int level = q.front().second;
-            q.pop();
+        v3 lo, hi;
+        aabb_par(objs, is_tri, lo, hi, nth);
+        create_node(std::move(objs), std::move(is_tri), 0, lo, hi);
+        // the reference's FIFO queue, one level at a time: the nodes of a level are split in
+        // parallel, then their children are created in queue order (same node numbering)
+        std::vector<int> level_nodes{0};
+        int level = 0;
+        while (!level_nodes.empty()) {
             bvh.max_level_achieved = std::max(bvh.max_level_achieved, level);
-            std::vector<int> o = node_objs[ni];
-            std::vector<uint8_t> t = node_is_tri[ni];
-            if (bvh.nodes[ni].is_leaf) {
-                bvh.nodes[ni].children = o;
-                bvh.nodes[ni].is_triangle = t;
-                continue;
+            const int m = (int)level_nodes.size();
+            struct Split {
+                std::vector<int> lo_o, ro;
+                std::vector<uint8_t> lo_t, rt_;
+                v3 llo, lhi, rlo, rhi;
+            };
+            std::vector<Split> sp(m);
+            const int inner_threads = std::max(1, nth / std::max(1, m));
+            parallel_for(m, nth, [&](int j) {
+                const int ni = level_nodes[j];
+                if (bvh.nodes[ni].is_leaf) return;
+                const std::vector<int>& o = node_objs[ni];
+                const std::vector<uint8_t>& t = node_is_tri[ni];
+                const int n = (int)o.size(), ch = 1 << 15, nch = (n + ch - 1) / ch;
+                std::vector<float> key(n);
+                parallel_for(nch, inner_threads, [&](int c) {
+                    for (int i = c * ch; i < std::min(n, (c + 1) * ch); ++i) key[i] = sort_attr(o[i], t[i] != 0, level + 1);
+                });
+                std::vector<int> order;
+                sort_order(key, order, inner_threads);
+                const int half = (n + 1) / 2;
+                Split& S = sp[j];
+                S.lo_o.resize(half);
+                S.lo_t.resize(half);
+                S.ro.resize(n - half);
+                S.rt_.resize(n - half);
+                parallel_for(nch, inner_threads, [&](int c) {
+                    for (int i = c * ch; i < std::min(n, (c + 1) * ch); ++i) {
+                        if (i < half) {
+                            S.lo_o[i] = o[order[i]];
+                            S.lo_t[i] = t[order[i]];
+                        } else {
+                            S.ro[i - half] = o[order[i]];
+                            S.rt_[i - half] = t[order[i]];
+                        }
+                    }
+                });
+                if (!S.lo_o.empty()) aabb_par(S.lo_o, S.lo_t, S.llo, S.lhi, inner_threads);
+                if (!S.ro.empty()) aabb_par(S.ro, S.rt_, S.rlo, S.rhi, inner_threads);
+            });
+            std::vector<int> next;
+            for (int j = 0; j < m; ++j) {
+                const int ni = level_nodes[j];
+                if (bvh.nodes[ni].is_leaf) {
+                    bvh.nodes[ni].children = node_objs[ni];
+                    bvh.nodes[ni].is_triangle = node_is_tri[ni];
+                    continue;
+                }
+                Split& S = sp[j];
+                if (!S.lo_o.empty()) {
+                    const int c = create_node(std::move(S.lo_o), std::move(S.lo_t), level + 1, S.llo, S.lhi);
+                    next.push_back(c);
+                    bvh.nodes[ni].children.push_back(c);
+                }
+                if (!S.ro.empty()) {
+                    const int c = create_node(std::move(S.ro), std::move(S.rt_), level + 1, S.rlo, S.rhi);
+                    next.push_back(c);
+                    bvh.nodes[ni].children.push_back(c);
+                }
             }
+            level_nodes.swap(next);
             ++level;
-            // sortObjects: std::sort of (attribute, position) pairs
-            std::vector<std::pair<float, int>> ai;
-            ai.reserve(o.size());
-            for (size_t i = 0; i < o.size(); ++i) ai.push_back({sort_attr(o[i], t[i] != 0, level), (int)i});
-            std::sort(ai.begin(), ai.end());
-            std::vector<int> so(o.size());
-            std::vector<uint8_t> st(o.size());
-            for (size_t i = 0; i < o.size(); ++i) {
-                so[i] = o[ai[i].second];
-                st[i] = t[ai[i].second];
-            }
-            const size_t half = (so.size() + 1) / 2;
-            std::vector<int> lo(so.begin(), so.begin() + half), ro(so.begin() + half, so.end());
-            std::vector<uint8_t> lt(st.begin(), st.begin() + half), rt_(st.begin() + half, st.end());
-            if (!lo.empty()) {
-                const int c = create_node(std::move(lo), std::move(lt), level);
-                q.push({c, level});
-                bvh.nodes[ni].children.push_back(c);
-            }
-            if (!ro.empty()) {
-                const int c = create_node(std::move(ro), std::move(rt_), level);
-                q.push({c, level});
-                bvh.nodes[ni].children.push_back(c);
-            }
         }
     }
 
@@ -195,35 +325,70 @@ struct Box {
 constexpr int kMaxDepth = 36;
 
 struct Bvh2Builder {
-    std::vector<Box> pbox;
-    std::vector<v3> cent;
-    std::vector<int> idx;
+    std::vector<Box>* pbox;
+    std::vector<v3>* cent;
+    std::vector<int>* idx;
     std::vector<Bvh2Node> nodes;
     int max_leaf;
     int max_depth = 0;
+    // the top of the tree is built sequentially; ranges reaching par_depth become tasks, built in
+    // parallel afterwards (each range is a disjoint slice of idx, so the result does not depend on
+    // the order the tasks run in)
+    int par_depth = -1;
+    struct Task {
+        int begin, end, depth;
+    };
+    std::vector<Task> tasks;
 
     struct Desc {
         int child;
         int count;
         Box box;
     };
+    static constexpr int kTaskMark = -1000000000;  // child = kTaskMark - task: filled in after the tasks
+    static constexpr int kParN = 1 << 17, kParChunk = 1 << 14;
 
     Desc build(int begin, int end, int depth) {
         max_depth = std::max(max_depth, depth);
-        Box box, cb;
-        for (int i = begin; i < end; ++i) {
-            box.grow(pbox[idx[i]]);
-            cb.grow(cent[idx[i]]);
-        }
+        const std::vector<Box>& pb = *pbox;
+        const std::vector<v3>& ce = *cent;
+        int* ix = idx->data();
         const int n = end - begin;
+        // ranges above kParN (the top levels, before the subtree tasks) run their O(n) passes on
+        // all host threads, in fixed chunks merged in order (deterministic)
+        const bool par = n > kParN && par_depth > 0;
+        const int nch = par ? (n + kParChunk - 1) / kParChunk : 1;
+        Box box, cb;
+        if (par) {
+            std::vector<Box> cbox(nch), ccb(nch);
+            parallel_for(nch, host_threads(), [&](int c) {
+                for (int i = begin + c * kParChunk; i < std::min(end, begin + (c + 1) * kParChunk); ++i) {
+                    cbox[c].grow(pb[ix[i]]);
+                    ccb[c].grow(ce[ix[i]]);
+                }
+            });
+            for (int c = 0; c < nch; ++c) {
+                box.grow(cbox[c]);
+                cb.grow(ccb[c]);
+            }
+        } else {
+            for (int i = begin; i < end; ++i) {
+                box.grow(pb[ix[i]]);
+                cb.grow(ce[ix[i]]);
+            }
+        }
         if (n <= max_leaf) return Desc{begin, n, box};
+        if (depth == par_depth) {
+            tasks.push_back(Task{begin, end, depth});
+            return Desc{kTaskMark - (int)(tasks.size() - 1), 0, box};
+        }
         int axis = 0;
         const v3 ext = cb.hi - cb.lo;
         if (ext.y > ext.x) axis = 1;
         if (ext.z > (axis == 0 ? ext.x : ext.y)) axis = 2;
         const float cmin = axis == 0 ? cb.lo.x : (axis == 1 ? cb.lo.y : cb.lo.z);
         const float cext = axis == 0 ? ext.x : (axis == 1 ? ext.y : ext.z);
-        auto cval = [&](int p) { return axis == 0 ? cent[p].x : (axis == 1 ? cent[p].y : cent[p].z); };
+        auto cval = [&](int p) { return axis == 0 ? ce[p].x : (axis == 1 ? ce[p].y : ce[p].z); };
         int mid = -1;
         // depth guard: median splits halve the range, so switching to them once
         // depth + ceil(log2(n / max_leaf)) reaches kMaxDepth bounds the tree depth (and the
@@ -240,10 +405,28 @@ struct Bvh2Builder {
                 int b = (int)((cval(p) - cmin) * scale);
                 return b < 0 ? 0 : (b >= NB ? NB - 1 : b);
             };
-            for (int i = begin; i < end; ++i) {
-                const int b = bin_of(idx[i]);
-                bb[b].grow(pbox[idx[i]]);
-                bc[b]++;
+            if (par) {
+                std::vector<std::array<Box, NB>> cbb(nch);
+                std::vector<std::array<int, NB>> cbc(nch);
+                parallel_for(nch, host_threads(), [&](int c) {
+                    cbc[c].fill(0);
+                    for (int i = begin + c * kParChunk; i < std::min(end, begin + (c + 1) * kParChunk); ++i) {
+                        const int b = bin_of(ix[i]);
+                        cbb[c][b].grow(pb[ix[i]]);
+                        cbc[c][b]++;
+                    }
+                });
+                for (int c = 0; c < nch; ++c)
+                    for (int b = 0; b < NB; ++b) {
+                        bb[b].grow(cbb[c][b]);
+                        bc[b] += cbc[c][b];
+                    }
+            } else {
+                for (int i = begin; i < end; ++i) {
+                    const int b = bin_of(ix[i]);
+                    bb[b].grow(pb[ix[i]]);
+                    bc[b]++;
+                }
             }
             float rarea[NB];
             int rcnt[NB];
@@ -272,9 +455,27 @@ struct Bvh2Builder {
             const float leaf_cost = box.area() * n;
             const float split_cost = 0.5f * box.area() + best;  // traversal cost ~ half a triangle
             if (best_b > 0 && (split_cost < leaf_cost || n > 2 * max_leaf)) {
-                int* p = std::partition(idx.data() + begin, idx.data() + end,
-                                        [&](int q) { return bin_of(q) < best_b; });
-                mid = (int)(p - idx.data());
+                if (par) {  // stable two-pass partition: per-chunk counts, then scatter in chunk order
+                    std::vector<int> nleft(nch + 1, 0), tmp(n);
+                    parallel_for(nch, host_threads(), [&](int c) {
+                        int k = 0;
+                        for (int i = begin + c * kParChunk; i < std::min(end, begin + (c + 1) * kParChunk); ++i)
+                            k += bin_of(ix[i]) < best_b;
+                        nleft[c + 1] = k;
+                    });
+                    for (int c = 0; c < nch; ++c) nleft[c + 1] += nleft[c];
+                    const int total_left = nleft[nch];
+                    parallel_for(nch, host_threads(), [&](int c) {
+                        int l = nleft[c], r = total_left + (c * kParChunk - nleft[c]);
+                        for (int i = begin + c * kParChunk; i < std::min(end, begin + (c + 1) * kParChunk); ++i)
+                            tmp[bin_of(ix[i]) < best_b ? l++ : r++] = ix[i];
+                    });
+                    std::copy(tmp.begin(), tmp.end(), ix + begin);
+                    mid = begin + total_left;
+                } else {
+                    int* p = std::partition(ix + begin, ix + end, [&](int q) { return bin_of(q) < best_b; });
+                    mid = (int)(p - ix);
+                }
                 if (mid == begin || mid == end) mid = -1;
             } else if (best_b > 0) {
                 return Desc{begin, n, box};  // SAH prefers a leaf (n <= 2*max_leaf)
@@ -282,8 +483,7 @@ struct Bvh2Builder {
         }
         if (mid < 0) {  // median split (degenerate centroids or depth guard)
             mid = begin + n / 2;
-            std::nth_element(idx.data() + begin, idx.data() + mid, idx.data() + end,
-                             [&](int a, int b) { return cval(a) < cval(b); });
+            std::nth_element(ix + begin, ix + mid, ix + end, [&](int a, int b) { return cval(a) < cval(b); });
         }
         const int ni = (int)nodes.size();
         nodes.push_back(Bvh2Node{});
@@ -310,25 +510,28 @@ struct Bvh2Builder {
         }
     }
 };
+
 }  // namespace
 
 Bvh2 build_bvh2(const float* pos, int ntri, float eps, int max_leaf) {
     Bvh2 out;
     out.eps = eps;
-    Bvh2Builder b;
-    b.max_leaf = max_leaf;
-    b.pbox.resize(ntri);
-    b.cent.resize(ntri);
-    b.idx.resize(ntri);
-    for (int t = 0; t < ntri; ++t) {
-        Box bx;
-        for (int c = 0; c < 3; ++c) bx.grow(v3{pos[t * 9 + c * 3], pos[t * 9 + c * 3 + 1], pos[t * 9 + c * 3 + 2]});
-        bx.lo = bx.lo - splat(eps);
-        bx.hi = bx.hi + splat(eps);
-        b.pbox[t] = bx;
-        b.cent[t] = (bx.lo + bx.hi) * 0.5f;
-        b.idx[t] = t;
-    }
+    std::vector<Box> pbox(ntri);
+    std::vector<v3> cent(ntri);
+    std::vector<int> idx(ntri);
+    const int nth = host_threads();
+    const int chunk = 1 << 16;
+    parallel_for((ntri + chunk - 1) / chunk, nth, [&](int c) {
+        for (int t = c * chunk; t < std::min(ntri, (c + 1) * chunk); ++t) {
+            Box bx;
+            for (int k = 0; k < 3; ++k) bx.grow(v3{pos[t * 9 + k * 3], pos[t * 9 + k * 3 + 1], pos[t * 9 + k * 3 + 2]});
+            bx.lo = bx.lo - splat(eps);
+            bx.hi = bx.hi + splat(eps);
+            pbox[t] = bx;
+            cent[t] = (bx.lo + bx.hi) * 0.5f;
+            idx[t] = t;
+        }
+    });
     Bvh2Node empty{};
     for (int k = 0; k < 3; ++k) {
         empty.lo0[k] = empty.lo1[k] = FLT_MAX;
@@ -336,25 +539,67 @@ Bvh2 build_bvh2(const float* pos, int ntri, float eps, int max_leaf) {
     }
     empty.child[0] = empty.child[1] = -1;
     empty.count[0] = empty.count[1] = 0;
+    Bvh2Builder b;
+    b.pbox = &pbox;
+    b.cent = &cent;
+    b.idx = &idx;
+    b.max_leaf = max_leaf;
     if (ntri == 0) {
         b.nodes.push_back(empty);
     } else {
+        // the top levels sequentially, their subtrees (about 4 per thread) in parallel
+        b.par_depth = ntri >= (1 << 15) ? 1 + 6 : -1;
         b.nodes.push_back(empty);  // root slot 0
         // build children of the root directly so the root is always an inner node
         Bvh2Builder::Desc d = b.build(0, ntri, 1);
+        std::vector<Bvh2Builder> sub(b.tasks.size());
+        std::vector<Bvh2Builder::Desc> sub_root(b.tasks.size());
+        parallel_for((int)b.tasks.size(), nth, [&](int t) {
+            Bvh2Builder& s = sub[t];
+            s.pbox = &pbox;
+            s.cent = &cent;
+            s.idx = &idx;
+            s.max_leaf = max_leaf;
+            sub_root[t] = s.build(b.tasks[t].begin, b.tasks[t].end, b.tasks[t].depth);
+        });
+        // splice: task t's nodes follow the top nodes (and the earlier tasks'), child indices shifted
+        std::vector<int> base(b.tasks.size());
+        int total = (int)b.nodes.size();
+        for (size_t t = 0; t < sub.size(); ++t) {
+            base[t] = total;
+            total += (int)sub[t].nodes.size();
+            b.max_depth = std::max(b.max_depth, sub[t].max_depth);
+        }
+        auto resolve = [&](int& child, int& count) {
+            if (count == 0 && child <= Bvh2Builder::kTaskMark && child > Bvh2Builder::kTaskMark - (int)sub.size()) {
+                const int t = Bvh2Builder::kTaskMark - child;
+                child = sub_root[t].count > 0 ? sub_root[t].child : base[t] + sub_root[t].child;
+                count = sub_root[t].count;
+            }
+        };
+        for (Bvh2Node& nd : b.nodes)
+            for (int k = 0; k < 2; ++k) resolve(nd.child[k], nd.count[k]);
+        b.nodes.reserve(total);
+        for (size_t t = 0; t < sub.size(); ++t)
+            for (Bvh2Node nd : sub[t].nodes) {
+                for (int k = 0; k < 2; ++k)
+                    if (nd.count[k] == 0 && nd.child[k] >= 0) nd.child[k] += base[t];
+                b.nodes.push_back(nd);
+            }
+        if (d.count == 0 && d.child <= Bvh2Builder::kTaskMark) resolve(d.child, d.count);
         if (d.count > 0) {
             // the whole scene is one leaf: root = {leaf, empty}
             Bvh2Builder::Desc e{-1, 0, Box{}};
             b.set_node(0, d, e);
             b.nodes[0].child[1] = -1;
         } else {
-            // d.child is the index of the first pushed inner node (1): move it into slot 0
+            // d.child is the index of the first pushed inner node: move it into slot 0
             b.nodes[0] = b.nodes[d.child];
             b.nodes[d.child] = empty;  // dead slot (never referenced)
         }
     }
     out.nodes = std::move(b.nodes);
-    out.order = std::move(b.idx);
+    out.order = std::move(idx);
     out.max_depth = b.max_depth;
     return out;
 }
@@ -396,6 +641,11 @@ static float decode(float origin, int e, uint32_t q) {
 }
 }  // namespace
 
+void parallel_chunks(int n, int chunk, const std::function<void(int, int)>& f) {
+    const int nch = (n + chunk - 1) / chunk;
+    parallel_for(nch, host_threads(), [&](int c) { f(c * chunk, std::min(n, (c + 1) * chunk)); });
+}
+
 Bvh8 build_bvh8(const Bvh2& b2, int width) {
     Bvh8 out;
     if (width < 2 || width > 8) throw std::runtime_error("BVH8 width must be 2..8");
@@ -405,93 +655,138 @@ Bvh8 build_bvh8(const Bvh2& b2, int width) {
         int slot;   // BVH8 node index
         int depth;
     };
-    std::vector<Item> queue;
-    queue.push_back({0, 0, 1});
+    // breadth first, one level at a time: the nodes of a level are collapsed and quantised in
+    // parallel, then their inner children (contiguous, in slot order) and leaf records are numbered
+    // in level order -- the layout of the sequential breadth-first walk
+    struct Done {
+        Child2 ch[8];
+        int nch = 0, n_inner = 0, n_rec = 0;
+        uint32_t w[32];
+    };
+    const int nth = host_threads();
+    std::vector<Item> level{{0, 0, 1}};
     out.nodes.assign(32, 0u);
-    size_t head = 0;
-    while (head < queue.size()) {
-        const Item it = queue[head++];
-        out.max_depth = std::max(out.max_depth, it.depth);
-        std::vector<Child2> ch;
-        children_of(b2, it.node2, ch);
-        // greedy collapse: open the inner child with the largest surface area until `width` children
-        for (;;) {
-            if ((int)ch.size() >= width) break;
-            int best = -1;
-            float best_a = -1.0f;
-            for (size_t i = 0; i < ch.size(); ++i)
-                if (ch[i].count == 0 && area_of(ch[i]) > best_a) {
-                    best_a = area_of(ch[i]);
-                    best = (int)i;
+    while (!level.empty()) {
+        const int m = (int)level.size();
+        std::vector<Done> done(m);
+        std::vector<std::string> err(m);
+        parallel_for((m + 255) / 256, nth, [&](int blk) {
+            for (int j = blk * 256; j < std::min(m, (blk + 1) * 256); ++j) {
+                Done& D = done[j];
+                std::vector<Child2> ch;
+                children_of(b2, level[j].node2, ch);
+                // greedy collapse: open the inner child with the largest surface area until `width` children
+                for (;;) {
+                    if ((int)ch.size() >= width) break;
+                    int best = -1;
+                    float best_a = -1.0f;
+                    for (size_t i = 0; i < ch.size(); ++i)
+                        if (ch[i].count == 0 && area_of(ch[i]) > best_a) {
+                            best_a = area_of(ch[i]);
+                            best = (int)i;
+                        }
+                    if (best < 0) break;
+                    std::vector<Child2> sub;
+                    children_of(b2, ch[best].child, sub);
+                    if ((int)(ch.size() - 1 + sub.size()) > width) break;
+                    ch.erase(ch.begin() + best);
+                    ch.insert(ch.end(), sub.begin(), sub.end());
                 }
-            if (best < 0) break;
-            std::vector<Child2> sub;
-            children_of(b2, ch[best].child, sub);
-            if ((int)(ch.size() - 1 + sub.size()) > width) break;
-            ch.erase(ch.begin() + best);
-            ch.insert(ch.end(), sub.begin(), sub.end());
-        }
-        uint32_t* w = out.nodes.data() + (size_t)it.slot * 32;
-        // node box = union of the children
-        float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
-        for (const Child2& c : ch)
-            for (int a = 0; a < 3; ++a) {
-                lo[a] = std::min(lo[a], c.lo[a]);
-                hi[a] = std::max(hi[a], c.hi[a]);
+                uint32_t* w = D.w;
+                std::memset(w, 0, sizeof(D.w));
+                // node box = union of the children
+                float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+                for (const Child2& c : ch)
+                    for (int a = 0; a < 3; ++a) {
+                        lo[a] = std::min(lo[a], c.lo[a]);
+                        hi[a] = std::max(hi[a], c.hi[a]);
+                    }
+                int e[3];
+                for (int a = 0; a < 3; ++a) {
+                    std::memcpy(&w[a], &lo[a], 4);
+                    const double ext = (double)hi[a] - (double)lo[a];
+                    // the smallest ex >= -126 with 65000 * 2^ex >= ext (frexp's guess, then the exact test)
+                    int ex = -126;
+                    if (ext > 0.0) {
+                        int fe = 0;
+                        std::frexp(ext / 65000.0, &fe);
+                        ex = std::max(-126, fe - 2);
+                    }
+                    while (ex < 127 && std::ldexp(65000.0, ex) < ext) ++ex;
+                    // the device forms 2^e * (1/d) with |1/d| <= 1e20: keep it finite
+                    if (ex > 40) err[j] = "BVH8: scene extent too large to quantise";
+                    e[a] = ex;
+                }
+                w[3] = (uint32_t)(e[0] + 127) | ((uint32_t)(e[1] + 127) << 8) | ((uint32_t)(e[2] + 127) << 16);
+                uint32_t imask = 0, lmask = 0, counts = 0;
+                uint16_t q[6][8];
+                for (int sl = 0; sl < 8; ++sl)
+                    for (int k = 0; k < 6; ++k) q[k][sl] = (k < 3) ? 65535 : 0;  // empty: inverted box
+                for (size_t sl = 0; sl < ch.size(); ++sl) {
+                    const Child2& c = ch[sl];
+                    for (int a = 0; a < 3; ++a) {
+                        const float scale = std::ldexp(1.0f, e[a]);
+                        long ql = (long)std::floor(((double)c.lo[a] - (double)lo[a]) / scale);
+                        long qh = (long)std::ceil(((double)c.hi[a] - (double)lo[a]) / scale);
+                        ql = std::max(0L, std::min(65535L, ql));
+                        qh = std::max(0L, std::min(65535L, qh));
+                        while (ql > 0 && decode(lo[a], e[a], (uint32_t)ql) > c.lo[a]) --ql;
+                        while (qh < 65535 && decode(lo[a], e[a], (uint32_t)qh) < c.hi[a]) ++qh;
+                        if (decode(lo[a], e[a], (uint32_t)ql) > c.lo[a] || decode(lo[a], e[a], (uint32_t)qh) < c.hi[a])
+                            err[j] = "BVH8 quantisation is not conservative";
+                        q[a][sl] = (uint16_t)ql;
+                        q[3 + a][sl] = (uint16_t)qh;
+                    }
+                    if (c.count > 0) {
+                        lmask |= 1u << sl;
+                        counts |= (uint32_t)c.count << (4 * sl);
+                        D.n_rec += c.count;
+                    } else {
+                        imask |= 1u << sl;
+                        D.n_inner++;
+                    }
+                    D.ch[sl] = c;
+                }
+                D.nch = (int)ch.size();
+                w[6] = imask | (lmask << 8);
+                w[7] = counts;
+                for (int k = 0; k < 6; ++k)
+                    for (int sl = 0; sl < 8; sl += 2)
+                        w[8 + k * 4 + sl / 2] = (uint32_t)q[k][sl] | ((uint32_t)q[k][sl + 1] << 16);
             }
-        int e[3];
-        for (int a = 0; a < 3; ++a) {
-            std::memcpy(&w[a], &lo[a], 4);
-            const double ext = (double)hi[a] - (double)lo[a];
-            int ex = -126;
-            while (ex < 127 && std::ldexp(65000.0, ex) < ext) ++ex;
-            // the device forms 2^e * (1/d) with |1/d| <= 1e20: keep it finite
-            if (ex > 40) throw std::runtime_error("BVH8: scene extent too large to quantise");
-            e[a] = ex;
+        });
+        for (const std::string& e : err)
+            if (!e.empty()) throw std::runtime_error(e);
+        // number the children and records in level order
+        std::vector<int> child_base(m), tri_base(m);
+        int nodes_total = (int)(out.nodes.size() / 32), rec_total = (int)out.order.size();
+        for (int j = 0; j < m; ++j) {
+            child_base[j] = nodes_total;
+            tri_base[j] = rec_total;
+            nodes_total += done[j].n_inner;
+            rec_total += done[j].n_rec;
         }
-        w[3] = (uint32_t)(e[0] + 127) | ((uint32_t)(e[1] + 127) << 8) | ((uint32_t)(e[2] + 127) << 16);
-        uint32_t imask = 0, lmask = 0, counts = 0;
-        const int child_base = (int)(out.nodes.size() / 32);
-        const int tri_base = (int)out.order.size();
-        w[4] = (uint32_t)child_base;
-        w[5] = (uint32_t)tri_base;
-        int n_inner = 0;
-        uint16_t q[6][8];
-        for (int s = 0; s < 8; ++s)
-            for (int k = 0; k < 6; ++k) q[k][s] = (k < 3) ? 65535 : 0;  // empty: inverted box
-        for (size_t s = 0; s < ch.size(); ++s) {
-            const Child2& c = ch[s];
-            for (int a = 0; a < 3; ++a) {
-                const float scale = std::ldexp(1.0f, e[a]);
-                long ql = (long)std::floor(((double)c.lo[a] - (double)lo[a]) / scale);
-                long qh = (long)std::ceil(((double)c.hi[a] - (double)lo[a]) / scale);
-                ql = std::max(0L, std::min(65535L, ql));
-                qh = std::max(0L, std::min(65535L, qh));
-                while (ql > 0 && decode(lo[a], e[a], (uint32_t)ql) > c.lo[a]) --ql;
-                while (qh < 65535 && decode(lo[a], e[a], (uint32_t)qh) < c.hi[a]) ++qh;
-                if (decode(lo[a], e[a], (uint32_t)ql) > c.lo[a] || decode(lo[a], e[a], (uint32_t)qh) < c.hi[a])
-                    throw std::runtime_error("BVH8 quantisation is not conservative");
-                q[a][s] = (uint16_t)ql;
-                q[3 + a][s] = (uint16_t)qh;
-            }
-            if (c.count > 0) {
-                lmask |= 1u << s;
-                counts |= (uint32_t)c.count << (4 * s);
-                for (int r = c.child; r < c.child + c.count; ++r) out.order.push_back(b2.order[r]);
-            } else {
-                imask |= 1u << s;
-                n_inner++;
+        out.nodes.resize((size_t)nodes_total * 32, 0u);
+        out.order.resize(rec_total);
+        std::vector<Item> next;
+        next.reserve(nodes_total - (int)(out.nodes.size() / 32) + m * 8);
+        for (int j = 0; j < m; ++j) {
+            Done& D = done[j];
+            D.w[4] = (uint32_t)child_base[j];
+            D.w[5] = (uint32_t)tri_base[j];
+            std::memcpy(out.nodes.data() + (size_t)level[j].slot * 32, D.w, sizeof(D.w));
+            out.max_depth = std::max(out.max_depth, level[j].depth);
+            int rank = 0, r = tri_base[j];
+            for (int sl = 0; sl < D.nch; ++sl) {
+                const Child2& c = D.ch[sl];
+                if (c.count > 0) {
+                    for (int k = c.child; k < c.child + c.count; ++k) out.order[r++] = b2.order[k];
+                } else {
+                    next.push_back({c.child, child_base[j] + rank++, level[j].depth + 1});
+                }
             }
         }
-        w[6] = imask | (lmask << 8);
-        w[7] = counts;
-        for (int k = 0; k < 6; ++k)
-            for (int s = 0; s < 8; s += 2) w[8 + k * 4 + s / 2] = (uint32_t)q[k][s] | ((uint32_t)q[k][s + 1] << 16);
-        // allocate the inner children contiguously, in slot order
-        out.nodes.resize(out.nodes.size() + (size_t)n_inner * 32, 0u);
-        int rank = 0;
-        for (size_t s = 0; s < ch.size(); ++s)
-            if (ch[s].count == 0) queue.push_back({ch[s].child, child_base + rank++, it.depth + 1});
+        level.swap(next);
     }
     return out;
 }

@@ -10,6 +10,7 @@
 //    boxes inflated by `eps` so every point the reference's triangle test can accept lies inside.
 #pragma once
 #include <cstdint>
+#include <functional>
 #include <vector>
 
 #include "rt_math.h"
@@ -72,5 +73,8 @@ struct Bvh8 {
 };
 
 Bvh8 build_bvh8(const Bvh2& b2, int width = 8);
+
+// f(begin, end) over [0, n) in chunks of `chunk`, on the host's threads (scene upload loops)
+void parallel_chunks(int n, int chunk, const std::function<void(int, int)>& f);
 
 }  // namespace rt

@@ -8,8 +8,8 @@
 //   * float parsing = fast_atoreal_move<float>: float(intpart) + float(double(frac) * 10^-n)
 //   * one object (node) per 'o' and per changed 'g' name; one mesh per material inside an object
 //   * vertices are never shared between faces (one vertex per face corner, face order)
-//   * quads: fan from the concave corner (corner 0 for convex quads); n>4: fan (ear-cutting of
-//     Assimp is not restated -- none of the reference's data files have such faces)
+//   * quads: fan from the concave corner (corner 0 for convex quads); n>4: Assimp's ear cutting
+//     in the plane of the Newell normal (ear_cut; AndreasScene.obj and CGSceneAdv.obj have 107)
 //   * GenFaceNormals after Triangulate: meshes without 'vn' get per-triangle normals, a corner
 //     shared by two triangles keeps the last one written
 //   * materials: DefaultMaterial{kd .6, ks 0, Ns 0, d 1}; 'mtllib' leaves the last material of
@@ -17,6 +17,8 @@
 //   * node walk: root children are visited in reverse (std::stack), meshes of a node in order
 //   * transforms: identity matrices applied with glm's op order (-0 positions become +0;
 //     normals go through glm::inverseTranspose(mat3(I)), whose off-diagonals carry -0)
+#include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -435,6 +437,107 @@ struct AiMesh {
     int material = 0;
 };
 
+// TriangulateProcess for n > 4 (code/PostProcessing/TriangulateProcess.cpp, Assimp 5.0.1; the same
+// code as 3.3's): project onto the plane of the Newell normal (dropping the axis of its largest
+// component, axes swapped when that component is negative), then cut ears in polygon order -- an
+// ear is a convex corner (GetArea2D > 0 in double) whose triangle contains no other polygon point
+// (PointInTriangle2D on float dot products, open test, points equal to a corner skipped) -- and emit
+// the last three corners.  A polygon without an ear (not simple) keeps the triangles cut so far, as
+// Assimp does.
+static double area2d(const float* a, const float* b, const float* c) {  // GetArea2D(v1, v2, v3)
+    return 0.5 * (a[0] * ((double)c[1] - b[1]) + b[0] * ((double)a[1] - c[1]) + c[0] * ((double)b[1] - a[1]));
+}
+
+static bool point_in_triangle2d(const float* p0, const float* p1, const float* p2, const float* pp) {
+    const float v0[2] = {p1[0] - p0[0], p1[1] - p0[1]};
+    const float v1[2] = {p2[0] - p0[0], p2[1] - p0[1]};
+    const float v2[2] = {pp[0] - p0[0], pp[1] - p0[1]};
+    double dot00 = v0[0] * v0[0] + v0[1] * v0[1];  // aiVector2D operator* (float), then double
+    const double dot01 = v0[0] * v1[0] + v0[1] * v1[1];
+    const double dot02 = v0[0] * v2[0] + v0[1] * v2[1];
+    double dot11 = v1[0] * v1[0] + v1[1] * v1[1];
+    const double dot12 = v1[0] * v2[0] + v1[1] * v2[1];
+    const double inv_denom = 1 / (dot00 * dot11 - dot01 * dot01);
+    dot11 = (dot11 * dot02 - dot01 * dot12) * inv_denom;
+    dot00 = (dot00 * dot12 - dot01 * dot02) * inv_denom;
+    return (dot11 > 0) && (dot00 > 0) && (dot11 + dot00 < 1);
+}
+
+static void ear_cut(const std::vector<v3>& verts, const std::vector<uint32_t>& idx,
+                    std::vector<std::array<uint32_t, 3>>& tris) {
+    const int max = (int)idx.size();
+    // NewellNormal<3,3,3> (PolyTools.h): the first two points repeated at the end
+    std::vector<v3> p(max + 2);
+    for (int k = 0; k < max; ++k) p[k] = verts[idx[k]];
+    p[max] = p[0];
+    p[max + 1] = p[1];
+    float sum_xy = 0.0f, sum_yz = 0.0f, sum_zx = 0.0f;
+    for (int k = 0; k < max; ++k) {
+        sum_xy += p[k + 1].x * (p[k + 2].y - p[k].y);
+        sum_yz += p[k + 1].y * (p[k + 2].z - p[k].z);
+        sum_zx += p[k + 1].z * (p[k + 2].x - p[k].x);
+    }
+    const v3 n{sum_yz, sum_zx, sum_xy};
+    const float ax = n.x > 0 ? n.x : -n.x, ay = n.y > 0 ? n.y : -n.y, az = n.z > 0 ? n.z : -n.z;
+    int ac = 0, bc = 1;  // no z: project to xy
+    float inv = n.z;
+    if (ax > ay) {
+        if (ax > az) {  // no x: yz
+            ac = 1;
+            bc = 2;
+            inv = n.x;
+        }
+    } else if (ay > az) {  // no y: zx
+        ac = 2;
+        bc = 0;
+        inv = n.y;
+    }
+    if (inv < 0.0f) std::swap(ac, bc);
+    auto comp = [](const v3& v, int a) { return a == 0 ? v.x : (a == 1 ? v.y : v.z); };
+    std::vector<std::array<float, 2>> t(max);
+    std::vector<char> done(max, 0);
+    for (int k = 0; k < max; ++k) t[k] = {comp(verts[idx[k]], ac), comp(verts[idx[k]], bc)};
+    int num = max, ear = 0, prev = num - 1, next = 0;
+    while (num > 3) {
+        int num_found = 0;
+        for (ear = next;; prev = ear, ear = next) {
+            // break after two loops without a positive match
+            for (next = ear + 1; done[(next >= max ? next = 0 : next)]; ++next) {
+            }
+            if (next < ear) {
+                if (++num_found == 2) break;
+            }
+            const float *p1 = t[ear].data(), *p0 = t[prev].data(), *p2 = t[next].data();
+            // a convex corner: OnLeftSideOfLine2D(p0, p2, p1) is GetArea2D(p0, p1, p2) > 0
+            if (area2d(p0, p1, p2) > 0) continue;
+            int k = 0;
+            for (; k < max; ++k) {
+                const float* v = t[k].data();
+                auto same = [](const float* a, const float* b) { return a[0] == b[0] && a[1] == b[1]; };
+                if (!same(v, p1) && !same(v, p2) && !same(v, p0) && point_in_triangle2d(p0, p1, p2, v)) break;
+            }
+            if (k != max) continue;
+            break;  // an ear
+        }
+        if (num_found == 2) {  // no ear: not a simple polygon (Assimp logs and stops)
+            num = 0;
+            break;
+        }
+        tris.push_back({idx[prev], idx[ear], idx[next]});
+        done[ear] = 1;
+        --num;
+    }
+    if (num > 0) {
+        int k = 0;
+        while (done[k]) ++k;
+        const int a = k++;
+        while (done[k]) ++k;
+        const int b = k++;
+        while (done[k]) ++k;
+        tris.push_back({idx[a], idx[b], idx[k]});
+    }
+}
+
 // createTopology + createVertexArray + TriangulateProcess + GenFaceNormalsProcess
 static bool build_ai_mesh(const ObjModel& m, const ObjMesh& om, AiMesh& out) {
     if (om.faces.empty()) return false;
@@ -484,7 +587,7 @@ static bool build_ai_mesh(const ObjModel& m, const ObjMesh& om, AiMesh& out) {
             out.tris.push_back({poly[start], poly[(start + 1) % 4], poly[(start + 2) % 4]});
             out.tris.push_back({poly[start], poly[(start + 2) % 4], poly[(start + 3) % 4]});
         } else {
-            for (size_t i = 1; i + 1 < n; ++i) out.tris.push_back({poly[0], poly[i], poly[i + 1]});
+            ear_cut(out.verts, poly, out.tris);
         }
     }
     // GenFaceNormalsProcess (only meshes without normals)

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cfloat>
 #include <cmath>
 #include <cstdio>
@@ -53,6 +54,7 @@ struct rt_ctx {
     size_t wave_trace_bytes = 0;
     int wave_trace_n = 0;
     int job_trace_n = 0;
+    double create_ms[8] = {0};  // rt_create phases (rt_debug_create_ms)
     // view batch (rt_render_views_device): per-view cameras, 12 floats each
     float* d_views = nullptr;
     size_t views_bytes = 0;
@@ -259,7 +261,12 @@ static int upload_lights(rt_ctx* c, const rt_scene_desc* d) {
     return RT_OK;
 }
 
+static double ms_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
 extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
+    const auto t_start = std::chrono::steady_clock::now();
     if (!desc || !out) {
         set_error("rt_create: null argument");
         return RT_ERR_INVALID;
@@ -298,6 +305,7 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
     }
     c->ntri = ntri;
     c->nmesh = desc->num_meshes;
+    c->create_ms[0] = ms_since(t_start);  // validation + device
 
     // --- reference BVH (object order: triangles, then spheres) ---
     std::vector<float> sph4(desc->num_spheres * 4);
@@ -313,6 +321,7 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
         delete c;
         return RT_ERR_INVALID;
     }
+    c->create_ms[1] = ms_since(t_start);  // + reference BVH
     c->ref_nodes = (int)ref.nodes.size();
     c->ref_levels = ref.max_level_achieved + 1;
     if (c->ref_nodes > RT_MAX_REF_NODES) {
@@ -337,8 +346,14 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
 
     // --- binned-SAH BVH2 (boxes inflated by eps, DESIGN.md "conservative traversal") collapsed into
     // the quantised BVH8 the kernels walk ---
+    std::vector<float> chunk_max((ntri + (1 << 15) - 1) / (1 << 15) + 1, 8.0f);
+    parallel_chunks(ntri, 1 << 15, [&](int b, int e) {
+        float m = 8.0f;
+        for (size_t i = (size_t)b * 9; i < (size_t)e * 9; ++i) m = std::max(m, std::fabs(desc->positions[i]));
+        chunk_max[b >> 15] = m;
+    });
     float max_abs = 8.0f;
-    for (size_t i = 0; i < (size_t)ntri * 9; ++i) max_abs = std::max(max_abs, std::fabs(desc->positions[i]));
+    for (float m : chunk_max) max_abs = std::max(max_abs, m);
     const float eps = std::ldexp(max_abs, -16);
     Bvh8 bvh8;
     try {
@@ -349,6 +364,7 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
         delete c;
         return RT_ERR_INVALID;
     }
+    c->create_ms[2] = ms_since(t_start);  // + BVH2 / BVH8
     c->bvh8_depth = bvh8.max_depth;
     c->df_ok = bvh8.max_depth + 2 < RT_STACK8;  // else the whole-traversal kernel's deeper stack
     if (bvh8.max_depth + 2 >= RT_STACK_SIZE || (int)bvh8.order.size() != ntri) {
@@ -361,7 +377,8 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
 
     // --- triangle records (64 B) in BVH8 leaf order: v0|n.x, v1|n.y, v2|n.z, D|key_brute|key_bvh|ref_leaf ---
     std::vector<float> rec((size_t)ntri * 16);
-    for (int r = 0; r < ntri; ++r) {
+    parallel_chunks(ntri, 1 << 15, [&](int rb, int re) {
+    for (int r = rb; r < re; ++r) {
         const int t = bvh8.order[r];
         const float* p = desc->positions + (size_t)t * 9;
         const v3 v0{p[0], p[1], p[2]}, v1{p[3], p[4], p[5]}, v2{p[6], p[7], p[8]};
@@ -376,7 +393,9 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
         std::memcpy(&o[12], &D, 4);
         std::memcpy(&o[13], ib, 12);
     }
+    });
 
+    c->create_ms[3] = ms_since(t_start);  // + records
     bool all_opaque = true, glossy = false;
     std::vector<DMat> mats;
     device_materials(desc->materials, desc->num_meshes, mats, all_opaque, glossy);
@@ -419,6 +438,7 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
         }
     }
 
+    c->create_ms[4] = ms_since(t_start);  // + materials, textures
     DevScene& S = c->S;
     UP(reinterpret_cast<const float4*>(rec.data()), (size_t)ntri * 4, S.tri);
     UP(reinterpret_cast<const float4*>(bvh8.nodes.data()), bvh8.nodes.size() / 4, S.nodes);
@@ -443,6 +463,7 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
     S.nsph = desc->num_spheres;
     S.nref = (int)refn.size();
     S.all_opaque = all_opaque ? 1 : 0;
+    c->create_ms[5] = ms_since(t_start);  // + uploads
     int rc = upload_lights(c, desc);
     if (rc != RT_OK) {
         rt_destroy(c);
@@ -455,7 +476,16 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
         rt_destroy(c);
         return RT_ERR_HIP;
     }
+    c->create_ms[6] = ms_since(t_start);  // total
     *out = c;
+    return RT_OK;
+}
+
+// rt_create's phase clock (cumulative ms: device, reference BVH, BVH2/BVH8, records, materials and
+// textures, uploads, total)
+extern "C" int rt_debug_create_ms(rt_ctx* c, double* out, int n) {
+    if (!c || !out) return RT_ERR_INVALID;
+    for (int i = 0; i < n && i < 8; ++i) out[i] = c->create_ms[i];
     return RT_OK;
 }
 

@@ -128,7 +128,7 @@ EXPORTS = [
     "rt_destroy", "rt_render", "rt_render_device", "rt_render_views_device", "rt_render_views", "rt_unpermute_bands_device", "rt_intersect", "rt_shade",
     "rt_set_counting", "rt_debug_counters", "rt_ctx_info", "rt_selftest_math",
     "rt_postprocess_device", "rt_bitmap_device", "rt_postprocess", "rt_bitmap", "rt_encode_bmp", "rt_write_bmp",
-    "rt_philox4x32_10", "rt_debug_wave_trace", "rt_debug_job_trace", "rt_decode_png", "rt_ctx_set_option", "rt_texture_sample",
+    "rt_philox4x32_10", "rt_debug_wave_trace", "rt_debug_job_trace", "rt_debug_create_ms", "rt_decode_png", "rt_ctx_set_option", "rt_texture_sample",
     "rt_update_lights", "rt_update_materials", "rt_unpermute_views_device", "rt_scene_mesh_count", "rt_scene_mesh_get",
 ]
 
@@ -263,6 +263,7 @@ def lib():
                               C.c_int),
             "rt_debug_wave_trace": ([vp, P(C.c_uint64), C.c_int], C.c_int),
             "rt_debug_job_trace": ([vp, P(C.c_uint64), C.c_int], C.c_int),
+            "rt_debug_create_ms": ([vp, P(C.c_double), C.c_int], C.c_int),
             "rt_ctx_set_option": ([vp, C.c_int, C.c_int], C.c_int),
             "rt_texture_sample": ([vp, C.c_int, C.c_int, P(C.c_float), P(rt_params), P(C.c_float)], C.c_int),
             "rt_update_lights": ([vp, P(rt_scene_desc)], C.c_int),
@@ -462,6 +463,12 @@ class Context:
 
     def __del__(self):
         self.close()
+
+    def create_ms(self):
+        """rt_create's cumulative phase clock (ms): device, ref BVH, BVH2/8, records, materials, uploads, total."""
+        out = np.zeros(8, np.float64)
+        check(lib().rt_debug_create_ms(self.h, out.ctypes.data_as(C.POINTER(C.c_double)), 8))
+        return out[:7]
 
     def info(self):
         a, b, c, d = C.c_int(), C.c_int(), C.c_int(), C.c_int()
