@@ -10,27 +10,104 @@
 #include <string>
 #include <array>
 #include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <utility>
+
+#include <unistd.h>
 
 namespace rt {
 
 namespace {
-// run f(i) for i in [0, n) on up to `threads` host threads
+// run f(i) for i in [0, n) on up to `threads` host threads: a process-wide pool of workers started
+// once (scene uploads call this hundreds of times); a call made from inside a pool task runs inline
+class Pool {
+   public:
+    static Pool& get() {
+        // never destroyed (its workers may outlive static destructors); a forked child (no workers
+        // of its own) starts a new one
+        static Pool* p = nullptr;
+        static pid_t owner = 0;
+        static std::mutex m;
+        std::lock_guard<std::mutex> lk(m);
+        if (!p || owner != getpid()) {
+            p = new Pool();
+            owner = getpid();
+        }
+        return *p;
+    }
+    template <typename F>
+    void run(int n, int threads, F&& f) {
+        if (n <= 0) return;
+        if (threads <= 1 || n == 1 || tl_in_pool) {
+            for (int i = 0; i < n; ++i) f(i);
+            return;
+        }
+        std::lock_guard<std::mutex> one(call_);  // one parallel loop at a time
+        std::function<void(int)> fn = [&](int i) { f(i); };
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            job_ = &fn;
+            n_ = n;
+            next_ = 0;
+            active_ = std::min(threads, (int)workers_.size() + 1) - 1;
+            done_ = 0;
+            ++gen_;
+        }
+        cv_.notify_all();
+        tl_in_pool = true;
+        for (int i = next_++; i < n; i = next_++) fn(i);  // the caller works too
+        tl_in_pool = false;
+        std::unique_lock<std::mutex> lk(m_);
+        cv_done_.wait(lk, [&] { return done_ == active_; });
+        job_ = nullptr;
+    }
+
+   private:
+    Pool() {
+        const unsigned hc = std::thread::hardware_concurrency();
+        const int nw = (int)std::max(1u, std::min(hc == 0 ? 1u : hc, 16u)) - 1;
+        for (int w = 0; w < nw; ++w) workers_.emplace_back([this, w] { loop(w); });
+        for (std::thread& t : workers_) t.detach();
+    }
+    void loop(int w) {
+        tl_in_pool = true;
+        unsigned seen = 0;
+        for (;;) {
+            std::function<void(int)>* job;
+            int n;
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return gen_ != seen; });
+                seen = gen_;
+                if (w >= active_) continue;  // not needed for this loop
+                job = job_;
+                n = n_;
+            }
+            for (int i = next_++; i < n; i = next_++) (*job)(i);
+            {
+                std::lock_guard<std::mutex> lk(m_);
+                ++done_;
+            }
+            cv_done_.notify_one();
+        }
+    }
+    static thread_local bool tl_in_pool;
+    std::vector<std::thread> workers_;
+    std::mutex call_, m_;
+    std::condition_variable cv_, cv_done_;
+    std::function<void(int)>* job_ = nullptr;
+    int n_ = 0, active_ = 0, done_ = 0;
+    unsigned gen_ = 0;
+    std::atomic<int> next_{0};
+};
+thread_local bool Pool::tl_in_pool = false;
+
 template <typename F>
 void parallel_for(int n, int threads, F&& f) {
-    threads = std::max(1, std::min(threads, n));
-    if (threads == 1) {
-        for (int i = 0; i < n; ++i) f(i);
-        return;
-    }
-    std::atomic<int> next{0};
-    std::vector<std::thread> pool;
-    for (int t = 0; t < threads; ++t)
-        pool.emplace_back([&] {
-            for (int i = next++; i < n; i = next++) f(i);
-        });
-    for (std::thread& th : pool) th.join();
+    Pool::get().run(n, threads, std::forward<F>(f));
 }
 
 int host_threads() {
@@ -76,8 +153,11 @@ struct RefBuild {
         }
     }
 
+    std::vector<float> tkey[3];  // the three triangle attributes, precomputed (same float ops)
+
     float sort_attr(int obj, bool is_tri, int level) const {
         const int attr = level % 3;
+        if (is_tri && !tkey[attr].empty()) return tkey[attr][obj];
         if (is_tri) {
             const v3 a = vtx(obj, 0), b = vtx(obj, 1), c = vtx(obj, 2);
             if (attr == 0) return (a.x + b.x + c.x) / 3;
@@ -168,6 +248,15 @@ struct RefBuild {
 
     void build() {
         const int nth = host_threads();
+        for (int a = 0; a < 3; ++a) tkey[a].resize(ntri);
+        parallel_for((ntri + (1 << 15) - 1) >> 15, nth, [&](int c) {
+            for (int t = c << 15; t < std::min(ntri, (c + 1) << 15); ++t) {
+                const v3 a = vtx(t, 0), b = vtx(t, 1), cc = vtx(t, 2);
+                tkey[0][t] = (a.x + b.x + cc.x) / 3;
+                tkey[1][t] = (a.y + b.y + cc.y) / 3;
+                tkey[2][t] = (a.z + b.z + cc.z) / 3;
+            }
+        });
         std::vector<int> objs;
         std::vector<uint8_t> is_tri;
         objs.reserve(ntri + nsph);
@@ -548,7 +637,7 @@ Bvh2 build_bvh2(const float* pos, int ntri, float eps, int max_leaf) {
         b.nodes.push_back(empty);
     } else {
         // the top levels sequentially, their subtrees (about 4 per thread) in parallel
-        b.par_depth = ntri >= (1 << 15) ? 1 + 6 : -1;
+        b.par_depth = ntri >= (1 << 15) ? 1 + 8 : -1;
         b.nodes.push_back(empty);  // root slot 0
         // build children of the root directly so the root is always an inner node
         Bvh2Builder::Desc d = b.build(0, ntri, 1);
