@@ -1730,10 +1730,13 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
         if (PF && tracing && T.cur != RT_TRAV_NONE) node_fetch(S.nodes, T.cur, g);
         for (;;) {
             if (tracing) {
-                if (leaf_pending(T))
-                    trav_record<COUNT>(S, T, cnt);
-                else if (T.cur != RT_TRAV_NONE)
-                    trav_node<COUNT, 8, PF>(S, T, stk, g, cnt);
+                // a lane whose hit leaf slots are all taken (lh == 0) visits its next node in the
+                // same step as its current record (P.dual): both code paths run in every step a
+                // wave has lanes in each, so this fills lanes that would idle in one of them
+                const bool rec = leaf_pending(T);
+                if (rec) trav_record<COUNT>(S, T, cnt);
+                const bool nv = T.cur != RT_TRAV_NONE && (!rec || (P.dual && T.lh == 0u));
+                if (nv) trav_node<COUNT, 8, PF>(S, T, stk, g, cnt);
             }
             if (tracing && !leaf_pending(T) && T.cur == RT_TRAV_NONE) {
                 trav_finish(S, T);

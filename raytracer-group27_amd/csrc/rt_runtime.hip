@@ -67,6 +67,7 @@ struct rt_ctx {
     int opt_fan = 1;        // dynamic-fetch kernel: spherical-light samples as wave-shared fans
     int opt_interleave = -1;  // job -> pixel interleave: -1 by render shape, 0 off, 1 on
     int opt_fan_cap = 0;      // pixels a wave may have waiting on fans before it stops taking new ones (0: default)
+    int opt_dual = -1;        // dynamic-fetch steps: record and node visit in one iteration (-1 default, 0 off, 1 on)
     int opt_variant = -1;   // -1: the shipped variant for the render shape (RT_DF_BATCH / _FRAME, RT_WT_DEFAULT)
     char last_kernel[64] = {0};
 };
@@ -568,6 +569,10 @@ extern "C" int rt_ctx_set_option(rt_ctx* c, int option, int value) {
             if (value < -1 || value > 1) break;
             c->opt_interleave = value;
             return RT_OK;
+        case RT_OPT_DUAL_STEP:
+            if (value < -1 || value > 1) break;
+            c->opt_dual = value;
+            return RT_OK;
         case RT_OPT_FAN:
             if (value < 0 || value > 1) break;
             c->opt_fan = value;
@@ -824,6 +829,12 @@ static void shape_options(const rt_ctx* c, KParams& K) {
     // single frames with fans: a wave's jobs spread over 64 tiles (C4 52.9 -> 31.4 ms; the tile order
     // keeps its coherence elsewhere: C3 2.18 vs 2.41 ms, C2 0.77 vs 0.98 ms)
     K.interleave = c->opt_interleave >= 0 ? c->opt_interleave : (K.fan && K.n_views <= 1 ? 1 : 0);
+    // fan renders advance whole waves: the fans keep a wave's free lanes busy, so waiting for all 64
+    // costs little and each pass takes many new pixels (C4 single frame, refill 24 -> 64: 27.0 -> 13.2 ms)
+    if (K.fan && c->opt_refill == 0) K.refill = 64;
+    // (C3 16-view batch 0.81 -> 0.71 ms/frame, C4 single frame 13.1 -> 11.1 ms; a second record per
+    // step for lanes without a node visit measured slower: 0.72 / 11.4)
+    K.dual = c->opt_dual >= 0 ? c->opt_dual : 1;
 }
 
 static int launch_render(rt_ctx* c, KParams& K, hipStream_t st, int count_mode, rt_stats* stats) {

@@ -135,6 +135,7 @@ EXPORTS = [
 # rt_ctx_set_option (include/rt_amd.h): test / developer hooks; defaults are the shipped path
 OPT_KERNEL, OPT_COOP, OPT_COOP_MAX, OPT_REFILL, OPT_WAVE_TRACE, OPT_VARIANT, OPT_FAN, OPT_INTERLEAVE, OPT_FAN_CAP = \
     1, 2, 3, 4, 5, 6, 7, 8, 9
+OPT_DUAL_STEP = 10
 KERNEL_AUTO, KERNEL_WHOLE_TRAVERSAL, KERNEL_DYNAMIC_FETCH = 0, 1, 2
 # compiled kernel variants (rt_megakernel.hip RT_V_*, rt_runtime.hip RT_DF_* / RT_WT_*)
 V_CALL, V_NOPF, V_NOCOOP, V_W3, V_W4, V_W5 = 1, 2, 4, 8, 16, 128

@@ -16,7 +16,7 @@ for n in (64, 16, 4):
     q.sphere_light_ray_count = n
     for name, opts in arms:
         for k, v in {R.OPT_KERNEL: 0, R.OPT_VARIANT: -1, R.OPT_COOP: -1, R.OPT_COOP_MAX: 0, R.OPT_REFILL: 0,
-                     R.OPT_FAN: 1, R.OPT_INTERLEAVE: -1}.items():
+                     R.OPT_FAN: 1, R.OPT_INTERLEAVE: -1, R.OPT_FAN_CAP: 0, R.OPT_DUAL_STEP: -1}.items():
             ctx.set_option(k, v)
         for k, v in opts.items():
             ctx.set_option(k, v)

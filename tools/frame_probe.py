@@ -10,7 +10,7 @@ cfgs = [a for a in sys.argv[1:] if ":" not in a] or ["C3", "C4"]
 arms = [(a.split(":", 1)[0], {int(k): int(v) for k, v in (x.split("=") for x in a.split(":", 1)[1].split(",") if x)})
         for a in sys.argv[1:] if ":" in a] or [("default", {})]
 DEF = {R.OPT_KERNEL: 0, R.OPT_VARIANT: -1, R.OPT_COOP: -1, R.OPT_COOP_MAX: 0, R.OPT_REFILL: 0, R.OPT_FAN: 1,
-       R.OPT_INTERLEAVE: -1, R.OPT_FAN_CAP: 0}
+       R.OPT_INTERLEAVE: -1, R.OPT_FAN_CAP: 0, R.OPT_DUAL_STEP: -1}
 for cfg in cfgs:
     s, p, W, H, desc = R.build_config(cfg)
     ctx = R.Context(s)

@@ -24,7 +24,7 @@ for cfg in cfgs:
         cams = R.turntable_cameras(V, R.aspect_of(W, H))
         buf = torch.zeros(V * R.local_band_elems(W, H, 8, 1), dtype=torch.float32, device="cuda")
     for name, env in variants:
-        for k, v in {R.OPT_KERNEL: 0, R.OPT_VARIANT: -1, R.OPT_COOP: -1, R.OPT_COOP_MAX: 0, R.OPT_REFILL: 0, R.OPT_FAN: 1, R.OPT_INTERLEAVE: -1}.items():
+        for k, v in {R.OPT_KERNEL: 0, R.OPT_VARIANT: -1, R.OPT_COOP: -1, R.OPT_COOP_MAX: 0, R.OPT_REFILL: 0, R.OPT_FAN: 1, R.OPT_INTERLEAVE: -1, R.OPT_FAN_CAP: 0, R.OPT_DUAL_STEP: -1}.items():
             ctx.set_option(k, v)
         for k, v in env.items():
             ctx.set_option(int(k), int(v))
