@@ -99,13 +99,26 @@ __device__ __forceinline__ DMat render_mat(const DevScene& S, const Lane& L) {
 // the tree depth; a popped group's boxes are re-tested against the current best t and the
 // nearest survivor is visited next.  Every candidate is judged with the same reference
 // arithmetic and (t, key) order as trace_query.
+// A triangle record's 64 B in one memory round trip (PIN): without the pin the compiler sinks the
+// loads of D and the keys (r3) below the branches that use them, so a record costs three dependent
+// trips.  The 4-wave batch variant keeps the sunk loads (its waves hide the latency, and the pinned
+// registers cost it: C3 batch 0.69 vs 0.71 ms/frame); the others pin (C2 0.75 -> 0.72 ms).
+template <bool PIN = true>
+__device__ __forceinline__ void load_record(const float4* tp, float4& r0, float4& r1, float4& r2, float4& r3) {
+    r0 = tp[0];
+    r1 = tp[1];
+    r2 = tp[2];
+    r3 = tp[3];
+    if (PIN) asm volatile("" ::"v"(r3.x), "v"(r3.y), "v"(r3.z), "v"(r3.w));
+}
+
 template <bool COUNT>
 __device__ __forceinline__ bool test_records(const DevScene& S, int first, int count, v3 o, v3 d, v3 nd, float thr,
                                              bool REF, bool ANY, Best& best, RefMask& mask, float& tcull,
                                              bool& found, Cnt& cnt) {
     for (int r = first; r < first + count; ++r) {
-        const float4* tp = S.tri + r * 4;
-        const float4 r0 = tp[0], r1 = tp[1], r2 = tp[2], r3 = tp[3];
+        float4 r0, r1, r2, r3;
+        load_record(S.tri + r * 4, r0, r1, r2, r3);
         if (COUNT) {
             cnt.tris++;
             if (wave_leader()) cnt.wtris++;
@@ -1053,38 +1066,45 @@ __device__ __forceinline__ void trav_node(const DevScene& S, Trav& T, int* stk, 
     const float bx = pow2f(w3 & 0xFFu) * inv.x, by = pow2f((w3 >> 8) & 0xFFu) * inv.y,
                 bz = pow2f((w3 >> 16) & 0xFFu) * inv.z;
     const float ax = (f0.x - o.x) * inv.x, ay = (f0.y - o.y) * inv.y, az = (f0.z - o.z) * inv.z;
-    const uint32_t m = (T.cur & 0xFFu) & (imask | lmask);
+    const uint32_t m = (T.cur & 0xFFu) & (imask | lmask), mi = m & imask;
     const float tcull = T.tcull;
-    uint32_t hits = 0;
-    float tbest = FLT_MAX;
-    int sbest = -1;
+    // every slot tested without branches: a slot is hit iff max(t0, 0) <= min(t1, tcull) (= t0 <= t1,
+    // t1 >= 0, t0 <= tcull whenever a hit can still be accepted, tcull >= 0); the nearest inner hit
+    // is the minimum of (clamped t0's bits, slot) keys (ordering is free: results are order-independent)
+    // the near and far plane of an axis by the sign of its direction (fma is monotonic in the plane
+    // value: for b > 0 the lo plane gives the smaller t, for b < 0 the hi plane, for b == 0 both are a),
+    // so min/max per axis become one selection per plane word; near and far in one packed fma
+    const bool sx = __float_as_uint(inv.x) >> 31, sy = __float_as_uint(inv.y) >> 31, sz = __float_as_uint(inv.z) >> 31;
+    const float4 nx = sx ? qhx : qlx, fx = sx ? qlx : qhx, ny = sy ? qhy : qly, fy = sy ? qly : qhy,
+                 nz = sz ? qhz : qlz, fz = sz ? qlz : qhz;
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const f2 b2x = {bx, bx}, b2y = {by, by}, b2z = {bz, bz}, a2x = {ax, ax}, a2y = {ay, ay}, a2z = {az, az};
+    uint32_t hits = 0u, kbest = 0xFFFFFFFFu;
 #pragma unroll
     for (int s = 0; s < NW; ++s) {
-        if (m & (1u << s)) {
-            const int wi = s >> 1, sh = (s & 1) * 16;
-            auto q = [&](const float4& f) {
-                const uint32_t wv = __float_as_uint(wi == 0 ? f.x : wi == 1 ? f.y : wi == 2 ? f.z : f.w);
-                return (float)((wv >> sh) & 0xFFFFu);
-            };
-            const float tlx = fmaf(q(qlx), bx, ax), thx = fmaf(q(qhx), bx, ax);
-            const float tly = fmaf(q(qly), by, ay), thy = fmaf(q(qhy), by, ay);
-            const float tlz = fmaf(q(qlz), bz, az), thz = fmaf(q(qhz), bz, az);
-            const float t0 = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fminf(tlz, thz));
-            const float t1 = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fmaxf(tlz, thz));
-            if (t0 <= t1 && t1 >= 0.0f && t0 <= tcull) {
-                hits |= 1u << s;
-                if ((imask & (1u << s)) && (t0 < tbest || sbest < 0)) {
-                    tbest = t0;
-                    sbest = s;
-                }
-            }
-        }
+        const int wi = s >> 1, sh = (s & 1) * 16;
+        auto q = [&](const float4& n, const float4& f) {
+            const uint32_t wn = __float_as_uint(wi == 0 ? n.x : wi == 1 ? n.y : wi == 2 ? n.z : n.w);
+            const uint32_t wf = __float_as_uint(wi == 0 ? f.x : wi == 1 ? f.y : wi == 2 ? f.z : f.w);
+            return f2{(float)((wn >> sh) & 0xFFFFu), (float)((wf >> sh) & 0xFFFFu)};
+        };
+        const f2 tx = __builtin_elementwise_fma(q(nx, fx), b2x, a2x);  // (near, far)
+        const f2 ty = __builtin_elementwise_fma(q(ny, fy), b2y, a2y);
+        const f2 tz = __builtin_elementwise_fma(q(nz, fz), b2z, a2z);
+        const float t0 = fmaxf(fmaxf(tx.x, ty.x), fmaxf(tz.x, 0.0f));
+        const float t1 = fminf(fminf(tx.y, ty.y), fminf(tz.y, tcull));
+        const bool h = t0 <= t1;
+        hits |= h ? (1u << s) : 0u;
+        const uint32_t key = (__float_as_uint(t0) & ~7u) | (uint32_t)s;
+        kbest = (h && (mi & (1u << s))) ? min(kbest, key) : kbest;
     }
+    hits &= m;
     T.lb = __float_as_uint(f1.y);
     T.lc = __float_as_uint(f1.w);
     T.lh = hits & lmask;
     const uint32_t ih = hits & imask;
     if (ih) {
+        const uint32_t sbest = kbest & 7u;
         const uint32_t rest = ih & ~(1u << sbest);
         if (rest) {
             stk[T.sp * RT_WAVE] = (int)((node << 8) | rest);
@@ -1104,7 +1124,7 @@ __device__ __forceinline__ void trav_node(const DevScene& S, Trav& T, int* stk, 
 // One postponed leaf record (the loop body of test_records).  The cursor moves to the next hit
 // leaf slot when the current range is used up.  Any-hit queries drop the rest of their work on
 // the first accepted candidate.
-template <bool COUNT>
+template <bool COUNT, bool PIN>
 __device__ __forceinline__ void trav_record(const DevScene& S, Trav& T, Cnt& cnt) {
     if (T.rk == 0) {
         const int s = __ffs(T.lh) - 1;
@@ -1119,8 +1139,8 @@ __device__ __forceinline__ void trav_record(const DevScene& S, Trav& T, Cnt& cnt
     const int r = T.rr;
     T.rr = r + 1;
     T.rk--;
-    const float4* tp = S.tri + r * 4;
-    const float4 r0 = tp[0], r1 = tp[1], r2 = tp[2], r3 = tp[3];
+    float4 r0, r1, r2, r3;
+    load_record<PIN>(S.tri + r * 4, r0, r1, r2, r3);
     if (COUNT) {
         cnt.tris++;
         if (wave_leader()) cnt.wtris++;
@@ -1339,8 +1359,8 @@ __device__ __forceinline__ uint2 coop_group_trace(const float4* __restrict__ nod
                 }
                 const int r = rr++;
                 --rk;
-                const float4* tp = tri + (size_t)r * 4;
-                const float4 r0 = tp[0], r1 = tp[1], r2 = tp[2], r3 = tp[3];
+                float4 r0, r1, r2, r3;
+                load_record(tri + (size_t)r * 4, r0, r1, r2, r3);
                 n.y++;
                 float t;
                 if (!tri_test(r0, r1, r2, r3, o, d, nd, t)) continue;
@@ -1734,7 +1754,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
                 // same step as its current record (P.dual): both code paths run in every step a
                 // wave has lanes in each, so this fills lanes that would idle in one of them
                 const bool rec = leaf_pending(T);
-                if (rec) trav_record<COUNT>(S, T, cnt);
+                if (rec) trav_record<COUNT, !(V & RT_V_W4)>(S, T, cnt);
                 const bool nv = T.cur != RT_TRAV_NONE && (!rec || (P.dual && T.lh == 0u));
                 if (nv) trav_node<COUNT, 8, PF>(S, T, stk, g, cnt);
             }

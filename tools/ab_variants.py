@@ -1,7 +1,7 @@
 """Developer tool: A/B of the compiled kernel variants and drain / refill options in ONE process on
 one GPU, rounds interleaved so clock drift hits every arm alike.  Per config: median kernel ms of a
 single frame and of a V-view turntable batch (rt_render_views_device), per arm.
-Usage: python tools/ab_variants.py [C3 C4 ...] [--views V] [--rounds N] [--arms name:k=v,k=v ...]
+Usage: python tools/ab_variants.py [C3 C4 ...] [--views V] [--rounds N] [--arms name:k=v,k=v ...] [--lib SO]
 (keys are rt_ctx_set_option options, e.g. 6=3 is RT_OPT_VARIANT 3; default arms: every compiled variant)."""
 import argparse
 import os
@@ -18,7 +18,10 @@ ap.add_argument("configs", nargs="*", default=["C3"])
 ap.add_argument("--views", type=int, default=16)
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--arms", nargs="*", default=None)
+ap.add_argument("--lib", default=None, help="another build of librt_amd.so (A/B of two builds: one run each)")
 args = ap.parse_args()
+if args.lib:
+    R.LIB_PATH = os.path.abspath(args.lib)
 
 DEFAULTS = {R.OPT_KERNEL: 0, R.OPT_VARIANT: -1, R.OPT_COOP: -1, R.OPT_COOP_MAX: 0, R.OPT_REFILL: 0, R.OPT_FAN: 1, R.OPT_INTERLEAVE: -1, R.OPT_FAN_CAP: 0, R.OPT_DUAL_STEP: -1}
 
