@@ -346,6 +346,17 @@ int rt_debug_job_trace(rt_ctx* ctx, uint64_t* out, int max_jobs);
 /* rt_create's phase clock, cumulative ms (device, reference BVH, BVH2/BVH8, records, materials and
  * textures, uploads, total): up to n doubles. */
 int rt_debug_create_ms(rt_ctx* ctx, double* out, int n);
+/* Where rt_create builds the acceleration structures (replaces BoundingVolumeHierarchy's constructor,
+ * src/bounding_volume_hierarchy.cpp:5-9,108-217): 0 (default) on the GPU from 65 536 triangles, on
+ * the host below; 1 always on the host; 2 always on the GPU (rt_create fails if the GPU path declines
+ * the scene).  Process-wide; applies to later rt_create calls. */
+int rt_set_build_mode(int mode);
+/* The context's build: out[0] 1 = built on the GPU, out[1] BVH2 nodes, out[2] BVH2 depth,
+ * out[3] BVH8 nodes (up to n ints). */
+int rt_debug_build_info(rt_ctx* ctx, int* out, int n);
+/* Triangle records [first, first + count) as the kernels read them: 16 floats each (v0, n.x, v1, n.y,
+ * v2, n.z, D, then scene index / reference-BVH key / reference leaf as int bits). */
+int rt_debug_records(rt_ctx* ctx, float* out, int first, int count);
 
 /* Introspection for tests / roofline accounting. */
 int rt_ctx_info(rt_ctx* ctx, int* num_nodes, int* num_tri_records, int* ref_bvh_nodes,

@@ -13,7 +13,7 @@ BUILD = os.path.join(HERE, "build")
 LIB = os.path.join(HERE, "librt_amd.so")
 
 HOST_SRCS = ["obj_loader.cpp", "scene.cpp", "bvh_build.cpp", "rt_api_host.cpp", "bmp.cpp", "png_decode.cpp"]
-HIP_SRCS = ["rt_runtime.hip", "rt_post.hip"]
+HIP_SRCS = ["rt_runtime.hip", "rt_post.hip", "rt_build.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("RT_OFFLOAD_ARCH", "gfx950")
 

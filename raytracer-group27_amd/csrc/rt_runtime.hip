@@ -19,6 +19,7 @@
 
 #include "../../include/rt_amd.h"
 #include "bvh_build.h"
+#include "rt_build.h"
 #include "rt_internal.h"
 #include "rt_kernels.hip"
 #include "rt_megakernel.hip"
@@ -29,6 +30,10 @@ using namespace rt;
 // scene is a handful of node visits and the per-step refill bookkeeping does not pay (measured on
 // MI355X, DESIGN.md section 6: C1/C2/C5 vs C3/C4)
 #define RT_DF_MIN_TRIANGLES 65536
+// scenes from this many triangles build their structures on the GPU (rt_build.hip); smaller ones, and
+// any scene the GPU path declines, on the host (bvh_build.cpp)
+#define RT_GPU_BUILD_MIN 65536
+static int g_build_mode = 0;  // rt_set_build_mode: 0 by size, 1 host, 2 GPU
 
 struct rt_ctx {
     int device = 0;
@@ -55,6 +60,7 @@ struct rt_ctx {
     int wave_trace_n = 0;
     int job_trace_n = 0;
     double create_ms[8] = {0};  // rt_create phases (rt_debug_create_ms)
+    int built_on_gpu = 0, bvh2_nodes = 0, bvh2_depth = 0;
     // view batch (rt_render_views_device): per-view cameras, 12 floats each
     float* d_views = nullptr;
     size_t views_bytes = 0;
@@ -314,15 +320,30 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
         for (int k = 0; k < 3; ++k) sph4[s * 4 + k] = desc->spheres[s].center[k];
         sph4[s * 4 + 3] = desc->spheres[s].radius;
     }
+    // the GPU build (rt_build.hip) for large scenes; the host builders otherwise
+    GpuBuild gbuild;
+    bool gpu_built = false;
+    double t_gpu = 0.0;
+    if (g_build_mode == 2 || (g_build_mode == 0 && ntri >= RT_GPU_BUILD_MIN)) {
+        std::string gerr;
+        t_gpu = ms_since(t_start);
+        gpu_built = gpu_build(desc->positions, ntri, sph4.data(), desc->num_spheres, gbuild, gerr);
+        if (!gpu_built && g_build_mode == 2) {
+            set_error("rt_create: " + gerr);
+            delete c;
+            return RT_ERR_INVALID;
+        }
+    }
     RefBvh ref;
     try {
-        ref = build_ref_bvh(desc->positions, ntri, sph4.data(), desc->num_spheres, 4);
+        if (gpu_built) ref = std::move(gbuild.ref);
+        else ref = build_ref_bvh(desc->positions, ntri, sph4.data(), desc->num_spheres, 4);
     } catch (const std::exception& ex) {
         set_error(std::string("rt_create: ") + ex.what());
         delete c;
         return RT_ERR_INVALID;
     }
-    c->create_ms[1] = ms_since(t_start);  // + reference BVH
+    c->create_ms[1] = gpu_built ? t_gpu + gbuild.ms[0] : ms_since(t_start);  // + reference BVH
     c->ref_nodes = (int)ref.nodes.size();
     c->ref_levels = ref.max_level_achieved + 1;
     if (c->ref_nodes > RT_MAX_REF_NODES) {
@@ -348,7 +369,7 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
     // --- binned-SAH BVH2 (boxes inflated by eps, DESIGN.md "conservative traversal") collapsed into
     // the quantised BVH8 the kernels walk ---
     std::vector<float> chunk_max((ntri + (1 << 15) - 1) / (1 << 15) + 1, 8.0f);
-    parallel_chunks(ntri, 1 << 15, [&](int b, int e) {
+    if (!gpu_built) parallel_chunks(ntri, 1 << 15, [&](int b, int e) {
         float m = 8.0f;
         for (size_t i = (size_t)b * 9; i < (size_t)e * 9; ++i) m = std::max(m, std::fabs(desc->positions[i]));
         chunk_max[b >> 15] = m;
@@ -357,28 +378,41 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
     for (float m : chunk_max) max_abs = std::max(max_abs, m);
     const float eps = std::ldexp(max_abs, -16);
     Bvh8 bvh8;
-    try {
-        const Bvh2 bvh = build_bvh2(desc->positions, ntri, eps, 4);
-        bvh8 = build_bvh8(bvh, 8);
-    } catch (const std::exception& ex) {
-        set_error(std::string("rt_create: ") + ex.what());
-        delete c;
-        return RT_ERR_INVALID;
+    if (gpu_built) {
+        c->allocs.push_back(gbuild.tri);
+        c->allocs.push_back(gbuild.nodes);
+        c->S.tri = static_cast<const float4*>(gbuild.tri);
+        c->S.nodes = static_cast<const float4*>(gbuild.nodes);
+        bvh8.max_depth = gbuild.max_depth;
+        c->built_on_gpu = 1;
+        c->bvh2_nodes = gbuild.bvh2_nodes;
+        c->bvh2_depth = gbuild.bvh2_depth;
+    } else {
+        try {
+            const Bvh2 bvh = build_bvh2(desc->positions, ntri, eps, 4);
+            bvh8 = build_bvh8(bvh, 8);
+            c->bvh2_nodes = (int)bvh.nodes.size();
+            c->bvh2_depth = bvh.max_depth;
+        } catch (const std::exception& ex) {
+            set_error(std::string("rt_create: ") + ex.what());
+            delete c;
+            return RT_ERR_INVALID;
+        }
     }
-    c->create_ms[2] = ms_since(t_start);  // + BVH2 / BVH8
+    c->create_ms[2] = gpu_built ? t_gpu + gbuild.ms[2] : ms_since(t_start);  // + BVH2 / BVH8
     c->bvh8_depth = bvh8.max_depth;
     c->df_ok = bvh8.max_depth + 2 < RT_STACK8;  // else the whole-traversal kernel's deeper stack
-    if (bvh8.max_depth + 2 >= RT_STACK_SIZE || (int)bvh8.order.size() != ntri) {
+    if (bvh8.max_depth + 2 >= RT_STACK_SIZE || (!gpu_built && (int)bvh8.order.size() != ntri)) {
         set_error("rt_create: BVH8 deeper than the traversal stack");
-        delete c;
+        rt_destroy(c);
         return RT_ERR_INVALID;
     }
-    c->nnodes = (int)(bvh8.nodes.size() / 32);
+    c->nnodes = gpu_built ? gbuild.nnodes : (int)(bvh8.nodes.size() / 32);
     c->nrec = ntri;
 
     // --- triangle records (64 B) in BVH8 leaf order: v0|n.x, v1|n.y, v2|n.z, D|key_brute|key_bvh|ref_leaf ---
-    std::vector<float> rec((size_t)ntri * 16);
-    parallel_chunks(ntri, 1 << 15, [&](int rb, int re) {
+    std::vector<float> rec(gpu_built ? 0 : (size_t)ntri * 16);
+    if (!gpu_built) parallel_chunks(ntri, 1 << 15, [&](int rb, int re) {
     for (int r = rb; r < re; ++r) {
         const int t = bvh8.order[r];
         const float* p = desc->positions + (size_t)t * 9;
@@ -396,7 +430,7 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
     }
     });
 
-    c->create_ms[3] = ms_since(t_start);  // + records
+    c->create_ms[3] = ms_since(t_start);  // + records (the GPU build's are made with its BVH8)
     bool all_opaque = true, glossy = false;
     std::vector<DMat> mats;
     device_materials(desc->materials, desc->num_meshes, mats, all_opaque, glossy);
@@ -441,8 +475,10 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
 
     c->create_ms[4] = ms_since(t_start);  // + materials, textures
     DevScene& S = c->S;
-    UP(reinterpret_cast<const float4*>(rec.data()), (size_t)ntri * 4, S.tri);
-    UP(reinterpret_cast<const float4*>(bvh8.nodes.data()), bvh8.nodes.size() / 4, S.nodes);
+    if (!gpu_built) {
+        UP(reinterpret_cast<const float4*>(rec.data()), (size_t)ntri * 4, S.tri);
+        UP(reinterpret_cast<const float4*>(bvh8.nodes.data()), bvh8.nodes.size() / 4, S.nodes);
+    }
     std::vector<float> uvz;
     const float* uvp = desc->texcoords;
     if (!uvp) {
@@ -479,6 +515,33 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
     }
     c->create_ms[6] = ms_since(t_start);  // total
     *out = c;
+    return RT_OK;
+}
+
+// developer / test hooks of the scene build (include/rt_amd.h)
+extern "C" int rt_set_build_mode(int mode) {
+    if (mode < 0 || mode > 2) {
+        set_error("rt_set_build_mode: mode must be 0 (by size), 1 (host) or 2 (GPU)");
+        return RT_ERR_INVALID;
+    }
+    g_build_mode = mode;
+    return RT_OK;
+}
+
+extern "C" int rt_debug_build_info(rt_ctx* c, int* out, int n) {
+    if (!c || !out) return RT_ERR_INVALID;
+    const int v[4] = {c->built_on_gpu, c->bvh2_nodes, c->bvh2_depth, c->nnodes};
+    for (int i = 0; i < n && i < 4; ++i) out[i] = v[i];
+    return RT_OK;
+}
+
+extern "C" int rt_debug_records(rt_ctx* c, float* out, int first, int count) {
+    if (!c || !out || first < 0 || count < 0 || first + count > c->nrec) {
+        set_error("rt_debug_records: range out of bounds");
+        return RT_ERR_INVALID;
+    }
+    if (count == 0) return RT_OK;
+    HIP_TRY(hipMemcpy(out, c->S.tri + (size_t)first * 4, (size_t)count * 64, hipMemcpyDeviceToHost));
     return RT_OK;
 }
 

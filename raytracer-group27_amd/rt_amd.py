@@ -128,9 +128,17 @@ EXPORTS = [
     "rt_destroy", "rt_render", "rt_render_device", "rt_render_views_device", "rt_render_views", "rt_unpermute_bands_device", "rt_intersect", "rt_shade",
     "rt_set_counting", "rt_debug_counters", "rt_ctx_info", "rt_selftest_math",
     "rt_postprocess_device", "rt_bitmap_device", "rt_postprocess", "rt_bitmap", "rt_encode_bmp", "rt_write_bmp",
-    "rt_philox4x32_10", "rt_debug_wave_trace", "rt_debug_job_trace", "rt_debug_create_ms", "rt_decode_png", "rt_ctx_set_option", "rt_texture_sample",
+    "rt_philox4x32_10", "rt_debug_wave_trace", "rt_debug_job_trace", "rt_debug_create_ms", "rt_set_build_mode", "rt_debug_build_info", "rt_debug_records", "rt_decode_png", "rt_ctx_set_option", "rt_texture_sample",
     "rt_update_lights", "rt_update_materials", "rt_unpermute_views_device", "rt_scene_mesh_count", "rt_scene_mesh_get",
 ]
+
+BUILD_AUTO, BUILD_HOST, BUILD_GPU = 0, 1, 2
+
+
+def set_build_mode(mode):
+    """rt_set_build_mode: where later rt_create calls build the acceleration structures."""
+    check(lib().rt_set_build_mode(int(mode)))
+
 
 # rt_ctx_set_option (include/rt_amd.h): test / developer hooks; defaults are the shipped path
 OPT_KERNEL, OPT_COOP, OPT_COOP_MAX, OPT_REFILL, OPT_WAVE_TRACE, OPT_VARIANT, OPT_FAN, OPT_INTERLEAVE, OPT_FAN_CAP = \
@@ -265,6 +273,9 @@ def lib():
             "rt_debug_wave_trace": ([vp, P(C.c_uint64), C.c_int], C.c_int),
             "rt_debug_job_trace": ([vp, P(C.c_uint64), C.c_int], C.c_int),
             "rt_debug_create_ms": ([vp, P(C.c_double), C.c_int], C.c_int),
+            "rt_set_build_mode": ([C.c_int], C.c_int),
+            "rt_debug_build_info": ([vp, P(C.c_int), C.c_int], C.c_int),
+            "rt_debug_records": ([vp, P(C.c_float), C.c_int, C.c_int], C.c_int),
             "rt_ctx_set_option": ([vp, C.c_int, C.c_int], C.c_int),
             "rt_texture_sample": ([vp, C.c_int, C.c_int, P(C.c_float), P(rt_params), P(C.c_float)], C.c_int),
             "rt_update_lights": ([vp, P(rt_scene_desc)], C.c_int),
@@ -306,7 +317,7 @@ class Scene:
         check(lib().rt_scene_new(C.byref(self.h)), "rt_scene_new")
 
     def __del__(self):
-        if getattr(self, "h", None) and self.h.value:
+        if getattr(self, "h", None) and self.h.value and callable(lib):  # (module teardown: lib is gone)
             lib().rt_scene_free(self.h)
             self.h = C.c_void_p()
 
@@ -470,6 +481,20 @@ class Context:
         out = np.zeros(8, np.float64)
         check(lib().rt_debug_create_ms(self.h, out.ctypes.data_as(C.POINTER(C.c_double)), 8))
         return out[:7]
+
+    def build_info(self):
+        """rt_debug_build_info: built on the GPU?, BVH2 nodes, BVH2 depth, BVH8 nodes."""
+        out = (C.c_int * 4)()
+        check(lib().rt_debug_build_info(self.h, out, 4))
+        return {"gpu": bool(out[0]), "bvh2_nodes": out[1], "bvh2_depth": out[2], "bvh8_nodes": out[3]}
+
+    def records(self, first=0, count=None):
+        """rt_debug_records: float32 [count, 16] triangle records in BVH8 leaf order."""
+        if count is None:
+            count = self.info()["tri_records"] - first
+        out = np.zeros((count, 16), np.float32)
+        check(lib().rt_debug_records(self.h, out.ctypes.data_as(C.POINTER(C.c_float)), first, count))
+        return out
 
     def info(self):
         a, b, c, d = C.c_int(), C.c_int(), C.c_int(), C.c_int()

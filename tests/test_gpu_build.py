@@ -1,0 +1,74 @@
+"""The GPU scene build (rt_build.hip) against the host builders (bvh_build.cpp): everything the
+renderer's results depend on must match bit for bit -- the reference BVH (node boxes, every
+triangle's tie-break key and leaf id, so every useBVH=true query), the records' plane data -- and
+frames rendered from either build are identical (the BVH2/BVH8 shapes may differ; boxes are
+conservative and hits are order-independent)."""
+import numpy as np
+import pytest
+
+import rt_amd as R
+
+pytestmark = pytest.mark.gpu
+
+
+def _ctx(scene, mode):
+    R.set_build_mode(mode)
+    try:
+        return R.Context(scene)
+    finally:
+        R.set_build_mode(R.BUILD_AUTO)
+
+
+def _by_scene_index(rec):
+    idx = rec[:, 13].view(np.int32)
+    return rec[np.argsort(idx, kind="stable")]
+
+
+@pytest.mark.parametrize("cfg", ["C2", "C5", "C3"])
+def test_gpu_build_matches_host(cfg):
+    s, p, W, H, _ = R.build_config(cfg)
+    host = _ctx(s, R.BUILD_HOST)
+    dev = _ctx(s, R.BUILD_GPU)
+    try:
+        assert not host.build_info()["gpu"] and dev.build_info()["gpu"]
+        hi, di = host.info(), dev.info()
+        assert hi["tri_records"] == di["tri_records"]
+        assert (hi["ref_bvh_nodes"], hi["ref_bvh_levels"]) == (di["ref_bvh_nodes"], di["ref_bvh_levels"])
+        # records: same set, bit for bit (scene index, plane, D, reference key and leaf)
+        hr, dr = _by_scene_index(host.records()), _by_scene_index(dev.records())
+        assert np.array_equal(hr.view(np.uint32), dr.view(np.uint32))
+        # frames: a band of rows from the middle of the image, full recursion, both builds
+        h = 64 if cfg != "C5" else 32
+        cam = R.camera_from_trackball(aspect=R.aspect_of(W, H))
+        img_h, st_h = host.render(cam, p, W // 8, h)
+        img_d, st_d = dev.render(cam, p, W // 8, h)
+        assert st_h.rays == st_d.rays
+        assert np.array_equal(img_h.view(np.uint32), img_d.view(np.uint32))
+        # useBVH=true intersect queries (reference BVH culling + DFS-rank ties) agree as well
+        rng = np.random.default_rng(7)
+        rays = np.zeros(4096, R.RAY_DTYPE)
+        d = rng.normal(size=(4096, 3)).astype(np.float32)
+        d /= np.linalg.norm(d, axis=1, keepdims=True)
+        rays["origin"] = rng.uniform(-1.2, 1.2, size=(4096, 3)).astype(np.float32)
+        rays["direction"] = d
+        rays["t"] = np.float32(3.4e38)
+        for use_bvh in (0, 1):
+            a = host.intersect(rays, use_bvh=use_bvh)
+            b = dev.intersect(rays, use_bvh=use_bvh)
+            assert np.array_equal(a.view(np.uint8), b.view(np.uint8))
+    finally:
+        host.close()
+        dev.close()
+
+
+def test_gpu_build_is_default_for_large_scenes_and_deterministic():
+    s, p, W, H, _ = R.build_config("C3")
+    a = R.Context(s)
+    b = R.Context(s)
+    try:
+        ia, ib = a.build_info(), b.build_info()
+        assert ia["gpu"] and ib["gpu"] and ia == ib
+        assert np.array_equal(a.records().view(np.uint32), b.records().view(np.uint32))
+    finally:
+        a.close()
+        b.close()
