@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
 #include <cfloat>
 #include <cmath>
 #include <string>
@@ -35,7 +36,10 @@ namespace gb {
 constexpr int NB = 32;          // SAH bins (bvh_build.cpp Bvh2Builder)
 constexpr int kMaxLeaf = 4;     // build_bvh2(..., max_leaf = 4)
 constexpr int kMaxDepth = 36;   // bvh_build.cpp kMaxDepth (median splits past the guard)
-constexpr int kSmall = 2048;    // ranges up to this size are built as whole subtrees by one wave
+#ifndef RT_KSMALL
+#define RT_KSMALL 512
+#endif
+constexpr int kSmall = RT_KSMALL;  // ranges up to this size are built as whole subtrees by one wave
 constexpr int kChunk = 4096;    // level-synchronous phase: triangles per workgroup
 constexpr int kBinW = 13;       // bin: count, box lo/hi, centroid lo/hi (ordered-uint min/max)
 constexpr int kStack = 48;      // subtree wave: pending ranges
@@ -240,13 +244,23 @@ __global__ void k_ref_leaves(const int* __restrict__ perm, int nobj, int ntri, c
         lo = gmin(smin, smax);
         hi = gmax(smin, smax);
     }
+    // a wave within one leaf (all but the <= 15 at leaf boundaries) reduces first: 16 boxes take the
+    // atomics of every object otherwise
+    uint32_t v[6] = {f2o(lo.x), f2o(lo.y), f2o(lo.z), f2o(hi.x), f2o(hi.y), f2o(hi.z)};
     uint32_t* lb = leaf_box + l * 6;
-    atomicMin(lb + 0, f2o(lo.x));
-    atomicMin(lb + 1, f2o(lo.y));
-    atomicMin(lb + 2, f2o(lo.z));
-    atomicMax(lb + 3, f2o(hi.x));
-    atomicMax(lb + 4, f2o(hi.y));
-    atomicMax(lb + 5, f2o(hi.z));
+    const int l0 = __shfl(l, 0);
+    if (__ballot(true) == ~0ull && __all(l == l0)) {  // (a full wave: the shuffles read every lane)
+        for (int o = 32; o > 0; o >>= 1)
+            for (int k = 0; k < 6; ++k) {
+                const uint32_t u = (uint32_t)__shfl_xor((int)v[k], o);
+                v[k] = k < 3 ? min(v[k], u) : max(v[k], u);
+            }
+        if ((threadIdx.x & 63) != 0) return;
+    }
+    for (int k = 0; k < 6; ++k) {
+        if (k < 3) atomicMin(lb + k, v[k]);
+        else atomicMax(lb + k, v[k]);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1085,6 +1099,11 @@ bool gpu_build(const float* h_pos, int ntri, const float* sph4, int nsph, GpuBui
     using namespace gb;
     const auto t0 = std::chrono::steady_clock::now();
     auto ms_now = [&] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
+#ifdef RT_BUILD_TRACE
+#define TRACE(tag) do { hipDeviceSynchronize(); fprintf(stderr, "build %-12s %7.2f ms\n", tag, ms_now()); } while (0)
+#else
+#define TRACE(tag) do { } while (0)
+#endif
     const int nobj = ntri + nsph;
     if (ntri < 16 || nobj < 16) {
         err = "GPU build: too few objects";
@@ -1108,8 +1127,10 @@ bool gpu_build(const float* h_pos, int ntri, const float* sph4, int nsph, GpuBui
     GB_ALLOC(attr);
     GB_CHECK(hipMemsetAsync(maxabs, 0, 4, st));
     k_max_abs<<<1024, 256, 0, st>>>(pos, (size_t)ntri * 9, maxabs);
+    TRACE("upload");
     k_prim_setup<<<grid(ntri, 256), 256, 0, st>>>(pos, ntri, maxabs, bmin, bmax, cent, attr);
     GB_CHECK(hipGetLastError());
+    TRACE("setup");
 
     // ---- 1. reference BVH ----
     unsigned long long *k0 = B.get<unsigned long long>(nobj), *k1 = B.get<unsigned long long>(nobj);
@@ -1138,6 +1159,7 @@ bool gpu_build(const float* h_pos, int ntri, const float* sph4, int nsph, GpuBui
     GB_ALLOC(v1);
     GB_ALLOC(hist);
     GB_ALLOC(hscan);
+    TRACE("ref alloc");
     for (int level = 0; level < 4; ++level) {  // the split levels 0..3; attribute (level + 1) % 3
         SegBounds sb;
         seg_bounds(nobj, level, sb);
@@ -1145,6 +1167,7 @@ bool gpu_build(const float* h_pos, int ntri, const float* sph4, int nsph, GpuBui
         // 32 attribute bits, then the segment (level <= 3: < 8 segments)
         radix_sort(k0, v0, k1, perm, k2, v1, nobj, level == 0 ? 32 : 40, hist, hscan, st);
     }
+    TRACE("ref sorts");
     {
         std::vector<uint32_t> init(16 * 6);
         for (int l = 0; l < 16; ++l)
@@ -1271,6 +1294,7 @@ bool gpu_build(const float* h_pos, int ntri, const float* sph4, int nsph, GpuBui
         }
         GB_CHECK(hipMemcpy(lt, &r, sizeof(LTask), hipMemcpyHostToDevice));
     }
+    TRACE("bvh2 root");
     int nlevel = 1;
     std::vector<LTask> htasks;
     while (nlevel > 0) {
@@ -1313,6 +1337,7 @@ bool gpu_build(const float* h_pos, int ntri, const float* sph4, int nsph, GpuBui
     Ctrs hc;
     GB_CHECK(hipMemcpyAsync(&hc, ctr, sizeof(Ctrs), hipMemcpyDeviceToHost, st));
     GB_CHECK(hipStreamSynchronize(st));
+    TRACE("bvh2 levels");
     if (hc.nsmall > 0) k_subtrees<<<grid(hc.nsmall, 4), 256, 0, st>>>(small, hc.nsmall, idx, idx2, bmin, bmax, cent,
                                                                       nodes2, ctr);
     GB_CHECK(hipGetLastError());
