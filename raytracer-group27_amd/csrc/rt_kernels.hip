@@ -99,7 +99,7 @@ struct KParams {
     unsigned long long* stats;  // rays, node visits, tri tests, hits, ..., UB-regime hits
     int refill;                 // dynamic-fetch kernel: waiting lanes that end a traversal phase
     int shade_level;            // rt_shade: recursion level of the explicit rays (getFinalColor's `level`)
-    int fan;                    // dynamic-fetch kernel: spherical-light samples traced as wave-shared fans
+    int fan;                    // dynamic-fetch kernel: bit 0 spherical-, bit 1 plane-light samples as wave-shared fans
     int interleave;             // job -> pixel: a wave's 64 jobs are one pixel of each of 64 tiles
     int fan_cap;                // ... a wave with this many pixels waiting on fans takes no new pixels
     int dual;                   // dynamic-fetch kernel: a lane testing a leaf's records also visits its next node

@@ -270,6 +270,14 @@ __device__ __forceinline__ bool trace_query8(const DevScene& S, v3 o, v3 d, floa
 // ---- light loop -----------------------------------------------------------------------------
 // cansee(hp, target) (src/shadow.cpp:32-40): queues the first segment, or returns false when the
 // loop condition distance > SHADOW_ERROR_OFFSET fails at once (cansee returns true, no intersect).
+// a finished fan (the kernel's FanTable): visibility bit s of sample s, and (scenes with transparent
+// materials) each sample's cansee intensity, both in sample order
+struct FanResult {
+    uint64_t vis;
+    const float* inten;  // LDS; null for opaque scenes (every intensity is 1)
+    bool done;           // the lane resumes from its fan (its own last query is not a cansee segment)
+};
+
 __device__ __forceinline__ bool start_cansee(Lane& L, v3 target, Query& q) {
     v3 d = target - L.hp;
     L.sdist = length(d);
@@ -312,7 +320,7 @@ __device__ __forceinline__ v3 sphere_perp(v3 hp, v3 lp, float radius) {
 // (valid when have_result).
 template <bool TEX>
 __device__ __forceinline__ bool advance_lights_body(const KParams& P, Lane& L, bool have_result, bool vis,
-                                                    uint64_t fanvis, Query& q) {
+                                                    FanResult fan, Query& q) {
     const DevScene& S = P.S;
     for (;;) {
         if (L.lt == L_POINT) {
@@ -348,12 +356,25 @@ __device__ __forceinline__ bool advance_lights_body(const KParams& P, Lane& L, b
             if (have_result) {
                 have_result = false;
                 if (L.ls == -2) {
-                    // the whole fan, traced by the wave (fan_sample_query): bit s of fanvis = sample s
-                    // visible, bit 0 the centre.  Opaque scene: every intensity is 1, so the loop's sums
-                    // below are these integer counts (exact in float)
-                    const float nv = (float)__popcll(fanvis >> 1);
-                    L.a0 = 1.0f + nv;
-                    L.a1 = (float)(fanvis & 1ull) + nv;
+                    // the whole fan, traced by the wave (fan_sample_query): bit s of fan.vis = sample s
+                    // visible, bit 0 the centre
+                    if (!fan.inten) {
+                        // opaque scene: every intensity is 1, so the loop's sums are these integer
+                        // counts (exact in float)
+                        const float nv = (float)__popcll(fan.vis >> 1);
+                        L.a0 = 1.0f + nv;
+                        L.a1 = (float)(fan.vis & 1ull) + nv;
+                    } else {
+                        // the loop's sums in its order: the centre's intensity (mutated even when
+                        // blocked), then each visible sample's
+                        L.a0 = fan.inten[0];
+                        L.a1 = (fan.vis & 1ull) ? 1.0f : 0.0f;
+                        for (int s = 1; s <= P.sl_m * P.sl_n; ++s)
+                            if ((fan.vis >> s) & 1ull) {
+                                L.a1 += 1.0f;
+                                L.a0 += fan.inten[s];
+                            }
+                    }
                     L.ls = P.sl_m * P.sl_n;
                 } else if (L.ls == -1) {
                     L.a0 = L.sI;  // intensitySum is the centre sample's intensity (mutated even if blocked)
@@ -383,7 +404,7 @@ __device__ __forceinline__ bool advance_lights_body(const KParams& P, Lane& L, b
                 L.ls = -1;
                 continue;
             }
-            if (L.ls == -1 && P.fan) {
+            if (L.ls == -1 && (P.fan & 1)) {
                 // fan request: the kernel traces the centre and every sample of this light from hp
                 // across the wave's lanes and resumes here with the visibility mask
                 L.ls = -2;
@@ -448,9 +469,38 @@ __device__ __forceinline__ bool advance_lights_body(const KParams& P, Lane& L, b
                 L.u0 = lpos;
                 if (dot(normalize(L.hp - (lpos + 0.5f * (w + h))), normal) > 0.0f) {
                     L.ls = 0;
+                    if (P.fan & 2) {
+                        // fan request: the kernel traces the light's k * k samples from hp across the
+                        // wave's lanes and resumes here with their visibility and intensities
+                        L.ls = -2;
+                        L.shadow = true;
+                        return true;
+                    }
                 } else {
                     L.ls = k * k;  // not in front of the light: no samples
                 }
+            } else if (have_result && L.ls == -2) {
+                // the whole fan: the loop's accumulation replayed in sample order (px stepped by the
+                // same additions), each visible sample with its traced intensity
+                have_result = false;
+                const v3 dx = (1.0f / (float)(k - 1)) * w, dy = (1.0f / (float)(k - 1)) * h;
+                for (int s = 0; s < k * k; ++s) {
+                    if ((fan.vis >> s) & 1ull) {
+                        const v3 px = L.u0;
+                        L.a3 += fan.inten ? fan.inten[s] : 1.0f;
+                        const float dn = dot(normalize(L.hp - px), normal);
+                        L.a0 += ((dn < 0.0f) ? 0.0f : dn) / length(L.hp - px);
+                        L.a1 += 1.0f;
+                        const float c2 = dot(lane_nR(L), normalize(px - L.hp));
+                        L.a2 = (L.a2 < c2) ? c2 : L.a2;
+                    }
+                    L.u0 = L.u0 + dx;
+                    if (s % k == k - 1) {
+                        L.u1 = L.u1 + dy;
+                        L.u0 = L.u1;
+                    }
+                }
+                L.ls = k * k;
             } else if (have_result) {
                 have_result = false;
                 if (vis) {
@@ -493,8 +543,8 @@ __device__ __forceinline__ bool advance_lights_body(const KParams& P, Lane& L, b
 // the light loop as its own function: fewer live registers in the caller
 template <bool TEX>
 __device__ __attribute__((noinline)) bool advance_lights_call(const void* ka, Lane& L, bool have_result, bool vis,
-                                                              uint64_t fanvis, Query& q) {
-    return advance_lights_body<TEX>(kernel_params(ka), L, have_result, vis, fanvis, q);
+                                                              FanResult fan, Query& q) {
+    return advance_lights_body<TEX>(kernel_params(ka), L, have_result, vis, fan, q);
 }
 
 
@@ -784,50 +834,56 @@ __device__ __forceinline__ bool start_job(const KParams& P, const JobSrc& J, Lan
     return true;
 }
 
+// One cansee segment finished (src/shadow.cpp:41-67): 1 visible, 0 blocked, 2 the next segment
+// (past a transparent surface, intensity attenuated) queued in q.
+__device__ __forceinline__ int cansee_step(const DevScene& S, Query& q, bool hit, const Best& b, float& sI,
+                                           float& sdist) {
+    if (S.all_opaque) return hit ? 0 : 1;
+    if (!hit || b.t > sdist - 2.0f * 0.0005f) return 1;
+    const Surf s = surface(S, q.o, q.d, b);
+    if (s.m.transp != 1.0f) {
+        sdist -= b.t;
+        const float c = fabsf(dot(q.d, s.n));
+        const float R0 = s.m.transp;
+        sI = (float)((double)sI * (1.0 - ((double)R0 + (double)(1.0f - R0) * pow((double)(1.0f - c), 5.0))));
+        if (sdist > 0.0005f) {
+            q.o = s.p + 0.0005f * q.d;
+            q.t = FLT_MAX;
+            return 2;
+        }
+        return 1;  // loop exit without an opaque blocker
+    }
+    return 0;
+}
+
+// ... out of line, for the kernel's fan samples in scenes with transparent materials
+__device__ __attribute__((noinline)) int cansee_step_call(const void* ka, Query& q, bool hit, const Best& b, float& sI,
+                                                          float& sdist) {
+    return cansee_step(kernel_params(ka).S, q, hit, b, sI, sdist);
+}
+
 // The state-machine advance after a finished query (q = that query's ray; hit, b = its result):
 // the cansee segment loop, the light loop, the recursion tree, the camera samples and the pixel
 // output.  Returns true with the next query in q (L.shadow says which kind); false when the lane's
 // job is complete (L.job = -1).
 template <bool COUNT, bool TEX>
 __device__ __forceinline__ bool advance_lane(const KParams& P, const JobSrc& J, const void* ka, Lane& L, Frame* fr,
-                                             bool hit, const Best& b, uint64_t fanvis, Query& q, Cnt& cnt,
+                                             bool hit, const Best& b, FanResult fan, Query& q, Cnt& cnt,
                                              uint32_t job_rays) {
     const DevScene& S = P.S;
     bool lights_have = false, lights_vis = false;
     if (L.shadow) {
-        // one cansee segment (src/shadow.cpp:41-67)
-        bool vis;
-        if (S.all_opaque) {
-            vis = !hit;
-        } else if (!hit || b.t > L.sdist - 2.0f * 0.0005f) {
-            vis = true;
-        } else {
-            const Surf s = surface(S, q.o, q.d, b);
-            if (s.m.transp != 1.0f) {
-                L.sdist -= b.t;
-                const float c = fabsf(dot(q.d, s.n));
-                const float R0 = s.m.transp;
-                L.sI = (float)((double)L.sI *
-                               (1.0 - ((double)R0 + (double)(1.0f - R0) * pow((double)(1.0f - c), 5.0))));
-                if (L.sdist > 0.0005f) {
-                    q.o = s.p + 0.0005f * q.d;  // the next segment, same direction
-                    q.t = FLT_MAX;
-                    return true;
-                }
-                vis = true;  // loop exit without an opaque blocker
-            } else {
-                vis = false;
-            }
-        }
+        const int r = fan.done ? 1 : cansee_step(S, q, hit, b, L.sI, L.sdist);
+        if (r == 2) return true;  // the next segment, same direction
         lights_have = true;
-        lights_vis = vis;
+        lights_vis = r == 1;
     } else if (hit) {
         begin_node<COUNT, TEX>(P, L, fr, q.o, q.d, b, cnt);
     }
     bool more;
     if (L.shadow || hit) {
         L.shadow = false;
-        if (advance_lights_call<TEX>(ka, L, lights_have, lights_vis, fanvis, q)) return true;
+        if (advance_lights_call<TEX>(ka, L, lights_have, lights_vis, fan, q)) return true;
         // every light done: the node's colour, then its mirror / reflected child
         L.acc = L.acc + L.w * L.color;
         if (L.desc) {
@@ -879,8 +935,8 @@ __device__ __forceinline__ bool advance_lane(const KParams& P, const JobSrc& J, 
 // between queries instead of in registers across the traversal loop (kernel variant bit RT_V_CALL).
 template <bool COUNT, bool TEX>
 __device__ __attribute__((noinline)) bool advance_lane_call(const void* ka, Lane& L, Frame* fr, bool hit, const Best& b,
-                                                            uint64_t fanvis, Query& q, Cnt& cnt, uint32_t job_rays) {
-    return advance_lane<COUNT, TEX>(kernel_params(ka), kernel_jobs(ka), ka, L, fr, hit, b, fanvis, q, cnt, job_rays);
+                                                            FanResult fan, Query& q, Cnt& cnt, uint32_t job_rays) {
+    return advance_lane<COUNT, TEX>(kernel_params(ka), kernel_jobs(ka), ka, L, fr, hit, b, fan, q, cnt, job_rays);
 }
 
 // Kernel variants (compile-time): bit 0 RT_V_CALL = state machine out of line (with RT_V_NOCOOP); bit 1 RT_V_NOPF = no node prefetch in the dynamic-fetch traversal; bit 2 RT_V_NOCOOP = no drain
@@ -899,12 +955,12 @@ __device__ __attribute__((noinline)) bool advance_lane_call(const void* ka, Lane
 
 template <bool COUNT, bool TEX, int V>
 __device__ __forceinline__ bool advance_v(const KParams& P, const JobSrc& J, const void* ka, Lane& L, Frame* fr,
-                                          bool hit, const Best& b, uint64_t fanvis, Query& q, Cnt& cnt,
+                                          bool hit, const Best& b, FanResult fan, Query& q, Cnt& cnt,
                                           uint32_t job_rays) {
     if constexpr ((V & RT_V_CALL) != 0)
-        return advance_lane_call<COUNT, TEX>(ka, L, fr, hit, b, fanvis, q, cnt, job_rays);
+        return advance_lane_call<COUNT, TEX>(ka, L, fr, hit, b, fan, q, cnt, job_rays);
     else
-        return advance_lane<COUNT, TEX>(P, J, ka, L, fr, hit, b, fanvis, q, cnt, job_rays);
+        return advance_lane<COUNT, TEX>(P, J, ka, L, fr, hit, b, fan, q, cnt, job_rays);
 }
 
 // ---- whole-traversal persistent kernel ------------------------------------------------------
@@ -967,7 +1023,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_kernel(KParams P
         if (!busy) continue;
         if (COUNT && wave_leader()) cnt.wadv++;
         // ---- advance the state machine until the next query ----
-        need_trace = advance_v<COUNT, TEX, V>(P, J, ka, L, fr, hit, b, 0ull, q, cnt, job_rays);
+        need_trace = advance_v<COUNT, TEX, V>(P, J, ka, L, fr, hit, b, FanResult{0ull, nullptr, false}, q, cnt, job_rays);
     }
     flush_counters<COUNT>(P, cnt);
     if (P.wave_trace && lane_id == 0) {  // wave trace: (start, end, jobs) per wave, 100 MHz clock
@@ -1487,16 +1543,32 @@ struct FanTable {
     int traced[FAN_SLOTS];  // samples that needed a query (the owner's ray count)
     int li[FAN_SLOTS];      // the spherical light
     float hx[FAN_SLOTS], hy[FAN_SLOTS], hz[FAN_SLOTS];  // the shading point
+    int plane[FAN_SLOTS];                               // 1: a plane light's k * k grid, 0: a spherical light
     unsigned long long vis[FAN_SLOTS];                  // bit s: sample s visible
+    float inten[FAN_SLOTS][64];                         // sample s's cansee intensity (transparent scenes)
 };
 
 // Sample s of a fan (0: the centre; s >= 1: the loop's sample ls = s - 1): the cansee query of
 // getSpherelights with the target the loop builds (its perp rotated once per finished spoke).
 // False when the target is within SHADOW_ERROR_OFFSET (visible without a query).
-__device__ __forceinline__ bool fan_sample_query(const KParams& P, v3 hp, int li, int s, Query& q, float& sdist) {
+__device__ __forceinline__ bool fan_sample_query(const KParams& P, v3 hp, int li, int plane, int s, Query& q,
+                                                 float& sdist) {
+    v3 target;
+    if (plane) {
+        // getPlaneLights' grid (src/shadow.cpp:259-299): row i = s / k, column j = s % k, px reached by
+        // the loop's additions (py += dy per row, px += dx per column)
+        const rt_plane_light pl = P.S.plane[li];
+        const int k = P.plane_k, i = s / k, j = s % k;
+        const v3 w = ld3(pl.width), h = ld3(pl.height);
+        const v3 dx = (1.0f / (float)(k - 1)) * w, dy = (1.0f / (float)(k - 1)) * h;
+        v3 py = ld3(pl.position);
+        for (int r = 0; r < i; ++r) py = py + dy;
+        target = py;
+        for (int c = 0; c < j; ++c) target = target + dx;
+    } else {
     const rt_spherical_light sl = P.S.sl[li];
     const v3 lp = ld3(sl.position);
-    v3 target = lp;
+    target = lp;
     if (s > 0) {
         const int m = P.sl_m, ls = s - 1, j = ls % m, k = ls / m;
         v3 u0 = sphere_perp(hp, lp, sl.radius);
@@ -1505,6 +1577,7 @@ __device__ __forceinline__ bool fan_sample_query(const KParams& P, v3 hp, int li
             for (int i = 0; i < k; ++i) u0 = mul(rot, u0);
         }
         target = lp + ((float)(m - j) / (float)m) * u0;
+    }
     }
     v3 d = target - hp;  // start_cansee
     sdist = length(d);
@@ -1518,8 +1591,9 @@ __device__ __forceinline__ bool fan_sample_query(const KParams& P, v3 hp, int li
 
 // a sample of fan slot f finished: into the fan's mask, then its count (the owner reads the mask
 // once the count is complete)
-__device__ __forceinline__ void fan_record(FanTable& ft, int f, int s, bool vis) {
+__device__ __forceinline__ void fan_record(FanTable& ft, int f, int s, bool vis, float inten) {
     if (vis) atomicOr(&ft.vis[f], 1ull << s);
+    ft.inten[f][s] = inten;
     atomicAdd(&ft.done[f], 1);
 }
 
@@ -1550,6 +1624,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
     int own_fan = -1;             // fan slot this lane's state machine waits for
     bool fan_req = false;         // the state machine posted a fan, no free slot yet
     int ray_fan = -1, ray_s = 0;  // the fan sample this lane's traversal slot traces
+    float ray_sI = 1.0f, ray_sdist = 0.0f;  // ... its cansee intensity and remaining distance
     Frame fr[RT_MAX_DEPTH];
     Lane L;
     L.job = -1;
@@ -1576,15 +1651,30 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
         // fan samples that finished: into their fan's mask
         if (FANS && pending && ray_fan >= 0) {
             pending = false;
-            fan_record(ft, ray_fan, ray_s, !T.found);
-            ray_fan = -1;
+            Query fq;
+            fq.o = T.o;
+            fq.d = T.d;
+            const int r = S.all_opaque ? (T.found ? 0 : 1) : cansee_step_call(ka, fq, T.found, T.best, ray_sI, ray_sdist);
+            if (r == 2) {  // past a transparent surface: the sample's next segment
+                q = fq;
+                start = true;
+                qshadow = true;
+                qsdist = ray_sdist;
+                atomicAdd(&ft.traced[ray_fan], 1);
+            } else {
+                fan_record(ft, ray_fan, ray_s, r == 1, ray_sI);
+                ray_fan = -1;
+            }
         }
         if (FANS) __syncthreads();
-        // the owners of complete fans resume with the mask
+        // the owners of complete fans resume with the mask -- once their own traversal slot is free (a
+        // lane waiting on its fan traces other fans' samples; its next query must not replace one)
         bool fan_done = false;
-        uint64_t fanvis = 0ull;
-        if (FANS && own_fan >= 0 && ft.done[own_fan] == ft.count[own_fan]) {
-            fanvis = ft.vis[own_fan];
+        FanResult fan{0ull, nullptr, false};
+        if (FANS && own_fan >= 0 && !tracing && !start && ft.done[own_fan] == ft.count[own_fan]) {
+            fan.vis = ft.vis[own_fan];
+            fan.inten = S.all_opaque ? nullptr : ft.inten[own_fan];
+            fan.done = true;
             job_rays += (uint32_t)ft.traced[own_fan];
             ft.owner[own_fan] = -1;
             own_fan = -1;
@@ -1596,7 +1686,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
             q.o = T.o;
             q.d = T.d;
             const int jb = L.job;
-            start = advance_v<COUNT, TEX, V>(P, J, ka, L, fr, T.found, T.best, fanvis, q, cnt, job_rays);
+            start = advance_v<COUNT, TEX, V>(P, J, ka, L, fr, T.found, T.best, fan, q, cnt, job_rays);
             if (P.job_trace && L.job == -1) {
                 P.job_trace[3 * jb + 1] = wall_clock64();
                 P.job_trace[3 * jb + 2] = job_rays;
@@ -1632,7 +1722,8 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
                         fq_in = 0;
                         ft.owner[f] = l;
                         ft.next[f] = 0;
-                        ft.count[f] = 1 + P.sl_m * P.sl_n;
+                        ft.plane[f] = L.lt == L_PLANE ? 1 : 0;
+                        ft.count[f] = L.lt == L_PLANE ? P.plane_k * P.plane_k : 1 + P.sl_m * P.sl_n;
                         ft.done[f] = 0;
                         ft.traced[f] = 0;
                         ft.vis[f] = 0ull;
@@ -1671,12 +1762,14 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
             }
             if (tfree && ray_fan >= 0) {
                 const v3 hp{ft.hx[ray_fan], ft.hy[ray_fan], ft.hz[ray_fan]};
-                if (fan_sample_query(P, hp, ft.li[ray_fan], ray_s, q, qsdist)) {
+                ray_sI = 1.0f;
+                if (fan_sample_query(P, hp, ft.li[ray_fan], ft.plane[ray_fan], ray_s, q, qsdist)) {
                     start = true;
                     qshadow = true;
+                    ray_sdist = qsdist;
                     atomicAdd(&ft.traced[ray_fan], 1);
                 } else {  // visible without a query
-                    fan_record(ft, ray_fan, ray_s, true);
+                    fan_record(ft, ray_fan, ray_s, true, 1.0f);
                     ray_fan = -1;
                 }
             }

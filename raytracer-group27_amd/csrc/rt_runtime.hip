@@ -653,11 +653,21 @@ extern "C" int rt_ctx_set_option(rt_ctx* c, int option, int value) {
 }
 
 
-// the kernel class a render runs: whole-traversal refill for small scenes, dynamic fetch for large
-static bool use_df(const rt_ctx* c) {
+// lights whose samples the dynamic-fetch kernel traces as wave-shared fans pay for that kernel on a
+// small scene too: at least 16 and at most 64 samples per spherical or plane light (C5, 3 plane lights of
+// 8 x 8 with a glass sphere: single frame 813 -> 351 ms, 4-view batch 218 -> 204 ms/frame)
+static bool fans_pay(const rt_ctx* c, const KParams& K) {
+    if (!c->opt_fan) return false;
+    const int ns = K.S.nsl > 0 ? 1 + K.sl_m * K.sl_n : 0, np = K.S.nplane > 0 ? K.plane_k * K.plane_k : 0;
+    return (ns >= 16 && ns <= 64) || (np >= 16 && np <= 64);
+}
+
+// the kernel class a render runs: whole-traversal refill for small scenes, dynamic fetch for large ones
+// and for sample-heavy lights
+static bool use_df(const rt_ctx* c, const KParams& K) {
     if (!c->df_ok || c->opt_kernel == RT_KERNEL_WHOLE_TRAVERSAL) return false;
     if (c->opt_kernel == RT_KERNEL_DYNAMIC_FETCH) return true;
-    return c->ntri >= RT_DF_MIN_TRIANGLES;
+    return c->ntri >= RT_DF_MIN_TRIANGLES || fans_pay(c, K);
 }
 
 // Kernel variants compiled (rt_megakernel.hip RT_V_*).  The dynamic-fetch class ships two, chosen by
@@ -704,7 +714,7 @@ static bool launch_shipped(bool df, int v, int grid, hipStream_t st, const KPara
 
 template <bool COUNT>
 static int launch_persistent(int grid, hipStream_t st, const KParams& K, const JobSrc& J, rt_ctx* c) {
-    const bool df = use_df(c);
+    const bool df = use_df(c, K);
     const bool tex = COUNT || K.S.tex_on;  // counting builds keep the texture code (one instance each)
     const int v = variant_of(c, df, K);
     bool ok = tex ? launch_shipped<COUNT, true>(df, v, grid, st, K, J) : launch_shipped<COUNT, false>(df, v, grid, st, K, J);
@@ -736,7 +746,7 @@ static int occupancy_of(int* per_cu) {
 
 // resident 64-lane blocks of the kernel (the persistent grid)
 static int persistent_grid(rt_ctx* c, const KParams& K) {
-    const bool df = use_df(c);
+    const bool df = use_df(c, K);
     const int v = variant_of(c, df, K);
     const int key = (df ? 512 : 0) + (v & 511);
     if (c->persistent_blocks[key] > 0) return c->persistent_blocks[key];
@@ -886,7 +896,12 @@ static void shape_options(const rt_ctx* c, KParams& K) {
     if (K.coop_max <= 0) K.coop = 0;
     // spherical lights as wave-shared fans (rt_megakernel.hip FanTable): dynamic-fetch kernel, opaque
     // scenes (every sample a plain any-hit query), at most 64 samples per light (one mask)
-    K.fan = (c->opt_fan && use_df(c) && K.S.all_opaque && K.S.nsl > 0 && 1 + K.sl_m * K.sl_n <= 64) ? 1 : 0;
+    // spherical lights (bit 0) and plane lights (bit 1) as wave-shared fans (rt_megakernel.hip FanTable):
+    // dynamic-fetch kernel, at most 64 samples per light (one mask); scenes with transparent materials
+    // carry each sample's intensity
+    const bool sph_fans = K.S.nsl > 0 && 1 + K.sl_m * K.sl_n <= 64;
+    const bool plane_fans = K.S.nplane > 0 && K.plane_k * K.plane_k <= 64;
+    K.fan = (c->opt_fan && use_df(c, K)) ? ((sph_fans ? 1 : 0) | (plane_fans ? 2 : 0)) : 0;
     if (c->opt_variant >= 0 && c->opt_variant != RT_DF_BATCH) K.fan = 0;  // fans are compiled into that variant only
     K.fan_cap = c->opt_fan_cap > 0 ? c->opt_fan_cap : 16;
     // single frames with fans: a wave's jobs spread over 64 tiles (C4 52.9 -> 31.4 ms; the tile order
@@ -914,7 +929,7 @@ static int launch_render(rt_ctx* c, KParams& K, hipStream_t st, int count_mode, 
         J.njobs = J.n_views * J.view_jobs;
         K.view_jobs = J.view_jobs;
         J.counter = reinterpret_cast<int*>(c->d_stats + 7);
-        J.xq = use_df(c) ? reinterpret_cast<int*>(c->d_stats + 16) : nullptr;
+        J.xq = use_df(c, K) ? reinterpret_cast<int*>(c->d_stats + 16) : nullptr;
         const int grid = (int)std::min<long long>(blocks * J.n_views, persistent_grid(c, K));
         if (c->opt_wave_trace) {
             const int rc = ensure(c, &c->d_wave_trace, &c->wave_trace_bytes,
@@ -1171,7 +1186,7 @@ extern "C" int rt_shade(rt_ctx* c, const rt_ray* rays, int n, const rt_params* p
         J.n_views = 1;
         J.view_jobs = n;
         J.counter = reinterpret_cast<int*>(c->d_stats + 7);
-        J.xq = use_df(c) ? reinterpret_cast<int*>(c->d_stats + 16) : nullptr;
+        J.xq = use_df(c, K) ? reinterpret_cast<int*>(c->d_stats + 16) : nullptr;
         const int grid = std::min((n + 63) / 64, persistent_grid(c, K));
         const int lrc = g_count_mode ? launch_persistent<true>(grid, c->stream, K, J, c)
                                      : launch_persistent<false>(grid, c->stream, K, J, c);

@@ -351,3 +351,46 @@ def test_sphere_light_fans_match_oracle(R, O, ctxs):
     rgb_ref, cnt_ref = O.Oracle(scene).shade(rays_in, prm)
     assert np.array_equal(got[1][1], cnt_ref)
     assert float(np.max(np.abs(got[1][0] - rgb_ref))) <= TOL
+
+
+def test_plane_and_transparent_fans_match_oracle(R, O):
+    """Plane-light grids and spherical lights in a scene with a transparent (glass) sphere, traced as
+    wave-shared fans: each sample runs its own cansee segment loop and hands back its intensity, and
+    the owner sums them in the loop's order -- the per-lane loop's bits and ray counts, and the oracle,
+    for frames and rt_shade."""
+    scene, prm, _, _, _ = R.build_config("C5")
+    scene.add_spherical_light((0.05, 0.5, 0.1), 0.08, (0.5, 0.5, 0.5))
+    prm.max_reflection_level = 3
+    prm.sphere_light_ray_count = 37
+    ctx = R.Context(scene)
+    try:
+        W, H = 48, 32
+        cam = R.camera_from_trackball(aspect=R.aspect_of(W, H))
+        out = {}
+        for fan in (1, 0):
+            with V.options(R, ctx, {R.OPT_KERNEL: R.KERNEL_DYNAMIC_FETCH, R.OPT_FAN: fan}):
+                out[fan] = ctx.render(cam, prm, W, H)
+        assert out[1][0].tobytes() == out[0][0].tobytes()
+        assert out[1][1].rays == out[0][1].rays
+        ref, rays = O.Oracle(scene).render(prm, W, H)
+        assert out[1][1].rays == rays
+        assert float(np.max(np.abs(out[1][0] - ref))) <= TOL
+        # rt_shade through the glass sphere and the box
+        rng = np.random.default_rng(11)
+        rays_in = np.zeros(192, R.RAY_DTYPE)
+        tgt = rng.uniform(-0.5, 0.5, (len(rays_in), 3)).astype(np.float32)
+        rays_in["origin"] = np.float32([0.0, 0.0, 2.5])
+        dirs = tgt - rays_in["origin"]
+        rays_in["direction"] = dirs / np.linalg.norm(dirs, axis=1, keepdims=True)
+        rays_in["t"] = np.float32(np.finfo(np.float32).max)
+        got = {}
+        for fan in (1, 0):
+            with V.options(R, ctx, {R.OPT_KERNEL: R.KERNEL_DYNAMIC_FETCH, R.OPT_FAN: fan}):
+                got[fan] = ctx.shade(rays_in, prm)
+        assert got[1][0].tobytes() == got[0][0].tobytes()
+        assert np.array_equal(got[1][1], got[0][1])
+        rgb_ref, cnt_ref = O.Oracle(scene).shade(rays_in, prm)
+        assert np.array_equal(got[1][1], cnt_ref)
+        assert float(np.max(np.abs(got[1][0] - rgb_ref))) <= TOL
+    finally:
+        ctx.close()
