@@ -269,7 +269,7 @@ def main():
         achieved = bytes0 / (avg_ms * 1e-3) / 1e9
         kname = st.kernel_name
         sha = lib_sha()
-        pmc, pmc_src = load_pmc(f"{args.config}/v{F}", kname, sha)
+        pmc, pmc_src = load_pmc(f"{args.config}v{F}", kname, sha)
         line = {
             "metric": METRIC,
             "value": total_rays / max_elapsed / 1e6,
