@@ -2,7 +2,7 @@
 
 Loads oracle/build/liboracle.so (CPU restatement of the reference hot path, ref_cpu.cpp).
 May be imported only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, as the
-checker or the timed CPU baseline.  Parity status: UNPINNED (see ref_cpu.cpp header).
+checker or the timed CPU baseline.  Parity status: pinned to the reference's render.bmp (see ref_cpu.cpp header).
 """
 import ctypes as C
 import os

@@ -12,7 +12,8 @@
 //   getPixel (black border)      src/screen.cpp:348-393
 // glm semantics: vec3 ops are per-component float ops; glm::dot = (x*x' + y*y') + z*z';
 // glm::exp/pow on float call expf/powf; vec3 /= int divides by float(int); glm::clamp = min(max).
-// Parity status: unpinned (glm 0.9.9.8 is not in the image; no reference test pins these).
+// Parity status: the Bloom option with the default box kernel is pinned by the reference's render.bmp
+// (tests/test_render_bmp_pin.py); the other options only by this restatement (glm 0.9.9.8 is not in the image).
 #include <algorithm>
 #include <cmath>
 #include <cstdint>

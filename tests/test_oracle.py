@@ -1,7 +1,7 @@
 """The CPU oracle (oracle/ref_cpu.cpp) against the committed golden vectors and against
-properties the reference's algorithm guarantees.  Parity to the reference binary is unpinned
-(no reference fixtures exist, the reference cannot be built here): these vectors were produced
-by tools/make_golden.py and pin the restatement against regressions."""
+properties the reference's algorithm guarantees.  These vectors were produced by
+tools/make_golden.py and pin the restatement against regressions; the pin to a reference-held
+output (render.bmp) is tests/test_render_bmp_pin.py."""
 import numpy as np
 import pytest
 

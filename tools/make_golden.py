@@ -2,8 +2,8 @@
 
 The reference ships no tests, golden vectors or fixtures for this path and cannot
 be built here, so these vectors are produced by the restatement itself: they pin the oracle
-(regression) and are what the GPU parity tests compare against.  Parity vs the reference binary
-stays UNPINNED.  Re-run after an intentional semantic change:
+(regression) and are what the GPU parity tests compare against.  The oracle itself is pinned to
+the reference's render.bmp (tests/test_render_bmp_pin.py).  Re-run after an intentional semantic change:
 
     python tools/make_golden.py
 """
