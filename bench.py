@@ -2,13 +2,14 @@
 
 Workload (config.workload): C3 = dragon proxy (800 000 triangles), 1920x1080,
 one point light, hard shadows + mirror recursion depth 4 (BASELINE.json configs[2]).  One step
-renders a batch of --views full frames (default 16: a turntable of the scene, 22.5 degrees apart) in
+renders a batch of --views full frames (default 64: a turntable of the scene, 5.625 degrees apart) in
 ONE launch of the persistent kernel (rt_render_views_device), each frame un-permuted into its own
 Screen::m_textureData image.  Inputs (scene, BVH) are resident in HBM before timing starts.
 
 N > 1 (one process per GPU, torch.distributed "nccl" = RCCL): the tile split of north_star.  Every
 rank renders its interleaved 8-row bands (band b -> rank b mod N) of ALL the step's views in one
-launch, the bands are all-gathered over xGMI and rank 0 un-permutes the views (one launch).  Per-step
+launch, the band buffers are gathered to rank 0 over xGMI (RCCL gather: every rank's buffer crosses
+its own link to rank 0, all links at once) and rank 0 un-permutes the views (one launch).  Per-step
 work is fixed as N grows ("scaling": "strong"), so N = 1 is exactly the BENCH workload.
 --partition frames instead gives each rank its own turntable views (no collective on the data path).
 
@@ -31,7 +32,7 @@ import numpy as np  # noqa: E402
 METRIC = "Mrays/s (primary+shadow+secondary) at 1920×1080; fraction of HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 BAND_ROWS = 8
-DEFAULT_VIEWS = 16  # frames per step: a 16-view turntable (22.5 deg apart) of the C3 scene in one launch
+DEFAULT_VIEWS = 64  # frames per step: a 64-view turntable (5.625 deg apart) of the C3 scene in one launch
 
 
 def algorithmic_bytes(st, pixels):
@@ -136,7 +137,7 @@ def main():
                     help="skip the single-frame latency record (profiling runs: one kernel shape only)")
     ap.add_argument("--partition", choices=("bands", "frames"), default="bands",
                     help="N>1: bands = every view of the step split into interleaved 8-row bands over the ranks, "
-                         "RCCL all-gather, un-permute on rank 0 (north_star's tile split, strong scaling); frames = "
+                         "RCCL gather to rank 0, un-permute there (north_star's tile split, strong scaling); frames = "
                          "every rank renders its own turntable views (weak scaling, no collective on the data path)")
     ap.add_argument("--views", type=int, default=DEFAULT_VIEWS,
                     help="frames per step, rendered in ONE launch (rt_render_views_device)")
@@ -188,7 +189,10 @@ def main():
     max_local = (nbands + b_count - 1) // b_count
     view_elems = max_local * BAND_ROWS * W * 3
     local_buf = torch.zeros(F * view_elems, dtype=torch.float32, device=dev)
-    gathered = torch.zeros(b_count * local_buf.numel(), dtype=torch.float32, device=dev) if b_count > 1 else local_buf
+    # RCCL: gather to rank 0; the gloo rehearsal (BENCH_DIST_BACKEND=gloo, device tensors) all-gathers instead
+    to_root = world > 1 and dist.get_backend() == "nccl"
+    gathered = (torch.zeros(b_count * local_buf.numel(), dtype=torch.float32, device=dev)
+                if rank == 0 or not to_root else None) if b_count > 1 else local_buf
     images = torch.zeros(F * W * H * 3, dtype=torch.float32, device=dev)
 
     # one explicit stream for render, gather and un-permute (torch's default stream is the null
@@ -199,7 +203,9 @@ def main():
         with torch.cuda.stream(bstream):
             st = ctx.render_views_device(cams, prm, W, H, BAND_ROWS, b_rank, b_count, local_buf.data_ptr(),
                                          bstream.cuda_stream)
-            if b_count > 1:
+            if b_count > 1 and to_root:  # to rank 0 only: each rank's bands cross one xGMI link, all at once
+                dist.gather(local_buf, gather_list=list(gathered.chunk(b_count)) if rank == 0 else None, dst=0)
+            elif b_count > 1:
                 dist.all_gather_into_tensor(gathered, local_buf)
             if rank == 0 or not bands:
                 R.check(R.lib().rt_unpermute_views_device(W, H, BAND_ROWS, b_count, F, R.C.c_void_p(gathered.data_ptr()),
@@ -288,7 +294,8 @@ def main():
                        "ms_per_frame": max_elapsed / args.steps / F * 1e3,
                        "rays_per_frame": int(total_rays / args.steps / (1 if bands else world) / F),
                        "band_rows": BAND_ROWS,
-                       "partition": (f"{world}-GPU tile split: interleaved 8-row bands of every view, RCCL all-gather"
+                       "partition": (f"{world}-GPU tile split: interleaved 8-row bands of every view, "
+                                     + ("RCCL gather to rank 0" if to_root else f"{dist.get_backend()} all-gather")
                                      if bands and world > 1 else
                                      f"{world} GPU(s), {F} whole frame(s) per GPU per step"),
                        "scene_upload_s": round(upload_s, 4),

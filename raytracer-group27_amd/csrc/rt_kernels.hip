@@ -143,6 +143,7 @@ struct Cnt {
     uint32_t wnodes, wtris, wadv;  // wave-level steps (counted by the first active lane): SIMD efficiency
     unsigned long long cyc_a, cyc_b;  // shader clocks per wave in the state machine / in traversal (df kernel)
     unsigned long long cyc_c, cyc_d;  // ... of cyc_a: advancing finished queries / fetching jobs
+    uint32_t hist[3];  // df kernel traversal iterations by tracing lanes 1-16 / 17-32 / 33-64 (leader)
 };
 
 // true on the lowest active lane of the wave (counting builds: one count per wave instruction stream)
@@ -562,6 +563,11 @@ __device__ void flush_counters(const KParams& P, const Cnt& c) {
         unsigned long long u = c.ub;
         for (int off = 32; off > 0; off >>= 1) u += __shfl_xor(u, off);
         if ((threadIdx.x & 63) == 0) atomicAdd(P.stats + 12, u);
+        for (int k = 0; k < 3; ++k) {
+            unsigned long long v = c.hist[k];
+            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+            if ((threadIdx.x & 63) == 0) atomicAdd(P.stats + 13 + k, v);
+        }
     }
 }
 

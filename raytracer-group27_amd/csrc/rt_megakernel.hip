@@ -1842,6 +1842,10 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
         float4 g[8];
         if (PF && tracing && T.cur != RT_TRAV_NONE) node_fetch(S.nodes, T.cur, g);
         for (;;) {
+            if (COUNT) {
+                const int ntr = __popcll(__ballot(tracing));  // (wave-wide: before the leader branch)
+                if (wave_leader()) cnt.hist[min((ntr - 1) >> 4, 2)]++;
+            }
             if (tracing) {
                 // a lane whose hit leaf slots are all taken (lh == 0) visits its next node in the
                 // same step as its current record (P.dual): both code paths run in every step a

@@ -119,10 +119,11 @@ def test_ranks_expand_scene_cache_concurrently(tmp_path):
             assert g.read() == h.read(), f
 
 
-def _views_worker(rank, world, port, W, H, band_rows, n_views, out_path):
+def _views_worker(rank, world, port, W, H, band_rows, n_views, out_path, to_root):
     """bench.py's N-rank step, with the oracle in place of the GPU: this rank's interleaved bands of
-    every view of the turntable batch, packed as rt_render_views_device packs them, all-gathered,
-    un-permuted on rank 0 (rt_unpermute_views_device's host statement)."""
+    every view of the turntable batch, packed as rt_render_views_device packs them, gathered to rank 0
+    (to_root: dist.gather into chunks of one buffer, bench.py's RCCL path) or all-gathered (its gloo
+    rehearsal), un-permuted on rank 0 (rt_unpermute_views_device's host statement)."""
     sys.path.insert(0, os.path.join(REPO, "raytracer-group27_amd"))
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
@@ -144,8 +145,11 @@ def _views_worker(rank, world, port, W, H, band_rows, n_views, out_path):
         local[v * per_view:v * per_view + rgb.size] = rgb.reshape(-1)
         rays += int(r.sum())
     t = torch.from_numpy(local)
-    gathered = torch.zeros(world * t.numel(), dtype=torch.float32)
-    dist.all_gather_into_tensor(gathered, t)
+    gathered = torch.zeros(world * t.numel(), dtype=torch.float32) if rank == 0 or not to_root else None
+    if to_root:
+        dist.gather(t, gather_list=list(gathered.chunk(world)) if rank == 0 else None, dst=0)
+    else:
+        dist.all_gather_into_tensor(gathered, t)
     total = torch.tensor([float(rays)], dtype=torch.float64)
     dist.all_reduce(total)
     if rank == 0:
@@ -155,8 +159,9 @@ def _views_worker(rank, world, port, W, H, band_rows, n_views, out_path):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("to_root", [True, False], ids=["gather", "all_gather"])
 @pytest.mark.parametrize("world,W,H,n_views", [(2, 20, 19, 3), (3, 16, 33, 2)])
-def test_band_split_of_view_batch_matches_single_renders(tmp_path, world, W, H, n_views):
+def test_band_split_of_view_batch_matches_single_renders(tmp_path, world, W, H, n_views, to_root):
     """The default N>1 bench layout (north_star's tile split of the benchmarked view batch): every
     gathered view equals the single-process render of that view, ray counts add up."""
     sys.path.insert(0, os.path.join(REPO, "raytracer-group27_amd"))
@@ -165,7 +170,7 @@ def test_band_split_of_view_batch_matches_single_renders(tmp_path, world, W, H, 
     import rt_amd as R
 
     out = str(tmp_path / "views.npz")
-    mp.start_processes(_views_worker, args=(world, _free_port(), W, H, 8, n_views, out), nprocs=world, join=True,
+    mp.start_processes(_views_worker, args=(world, _free_port(), W, H, 8, n_views, out, to_root), nprocs=world, join=True,
                        start_method="spawn")
     z = np.load(out)
     scene, prm, _, _, _ = R.build_config("C2")

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Rehearsal of bench.py's N-rank path on a one-GPU box: 2 ranks share the GPU over gloo
 # (the driver's multi-GPU runs use RCCL, one rank per GPU).  Default partition = the tile split
-# (bands of every view, all-gather, un-permute on rank 0); then the frames partition.
+# (bands of every view; gloo all-gathers where RCCL gathers to rank 0; un-permute on rank 0); then the frames partition.
 set -o pipefail
 mkdir -p gpurun_out
 export BENCH_DIST_BACKEND=gloo

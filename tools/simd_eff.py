@@ -40,5 +40,7 @@ for cfg in cfgs:
               f"eff_node={nodes / max(1, 64 * wn):.3f} eff_tri={tris / max(1, 64 * wt):.3f} "
               f"eff_adv={rays / max(1, 64 * wa):.3f} wave_steps/ray: node={wn / rays:.3f} tri={wt / rays:.3f} "
               f"adv={wa / rays:.3f} cycA={int(c[8]) / max(1, int(c[8]) + int(c[9])):.2f} "
-              f"(advance {int(c[10]) / max(1, int(c[8])):.2f}, job fetch {int(c[11]) / max(1, int(c[8])):.2f})", flush=True)
+              f"(advance {int(c[10]) / max(1, int(c[8])):.2f}, job fetch {int(c[11]) / max(1, int(c[8])):.2f}) "
+              f"iterations by tracing lanes 1-16/17-32/33-64: "
+              f"{[round(int(c[k]) / max(1, sum(int(c[j]) for j in (13, 14, 15))), 3) for k in (13, 14, 15)]}", flush=True)
     ctx.close()

@@ -24,8 +24,16 @@ for cfg in [a for a in sys.argv[1:] if a.startswith("C")] or ["C3"]:
     ctx = R.Context(s)
     ctx.set_option(R.OPT_WAVE_TRACE, 1)
     cam = R.camera_from_trackball(aspect=R.aspect_of(W, H))
-    ctx.render(cam, p, W, H)
-    _, st = ctx.render(cam, p, W, H)
+    V = int(os.environ.get("WT_VIEWS", "1"))  # > 1: a V-view turntable batch in one launch
+    if V > 1:
+        import torch
+        cams = R.turntable_cameras(V, R.aspect_of(W, H))
+        vb = torch.zeros(V * R.local_band_elems(W, H, 8, 1), dtype=torch.float32, device="cuda")
+        ctx.render_views_device(cams, p, W, H, 8, 0, 1, vb.data_ptr(), None)
+        st = ctx.render_views_device(cams, p, W, H, 8, 0, 1, vb.data_ptr(), None)
+    else:
+        ctx.render(cam, p, W, H)
+        _, st = ctx.render(cam, p, W, H)
     buf = np.zeros(8 * 65536, np.uint64)
     n = R.lib().rt_debug_wave_trace(ctx.h, buf.ctypes.data_as(C.POINTER(C.c_uint64)), 65536)
     t = buf[:8 * n].reshape(n, 8).astype(np.int64)
