@@ -11,4 +11,4 @@ cat gpurun_out/bench_${TAG}.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG} -o run -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-single-frame > gpurun_out/prof_${TAG}.log 2>&1 || exit $?
 find gpurun_out/prof_${TAG} -name "*stats*"
 [ "${2:-}" = "nopmc" ] && exit 0
-bash tools/profile.sh ${TAG} C3 16
+bash tools/profile.sh ${TAG} C3 64
