@@ -34,6 +34,10 @@ en_us = (jt[done, 1] - t0) / 100.0
 lat = en_us - st_us
 q = jt[done, 2]
 print(f"{cfg}: kernel {st.kernel_ms:.3f} ms, jobs {n}, traced {done.sum()}")
+if os.environ.get("JT_SAVE"):  # per-job (start us, end us, queries) for offline analysis
+    np.savez_compressed(os.environ["JT_SAVE"], start=((jt[:, 0] - t0) / 100.0).astype(np.float32),
+                        end=((jt[:, 1] - t0) / 100.0).astype(np.float32), queries=jt[:, 2].astype(np.int32),
+                        done=done, W=W, H=H)
 P = [0, 50, 90, 99, 99.9, 100]
 print("latency us pct", " ".join(f"{v:.1f}" for v in np.percentile(lat, P)))
 print("queries pct   ", " ".join(f"{v:.0f}" for v in np.percentile(q, P)))
