@@ -394,3 +394,39 @@ def test_plane_and_transparent_fans_match_oracle(R, O):
         assert float(np.max(np.abs(got[1][0] - rgb_ref))) <= TOL
     finally:
         ctx.close()
+
+
+def test_bench_step_c3_64_views(R, O, ctxs):
+    """The benchmarked step itself (bench.py defaults): C3 at 1920x1080, a 64-view turntable in ONE
+    rt_render_views_device launch, rebuilt by rt_unpermute_views_device.  Views 0, 21 and 63 are
+    bit-identical to single-frame renders with their cameras; the batch's ray count is the sum of the
+    64 single-frame counts; 256 pixels of view 21 (half of them on geometry) match the oracle."""
+    import torch
+
+    scene, ctx, prm, W, H = ctxs("C3")
+    F = 64
+    eulers = R.turntable_eulers(F)
+    cams = [R.camera_from_trackball(euler=e, aspect=R.aspect_of(W, H)) for e in eulers]
+    n = R.local_band_elems(W, H, 8, 1)
+    local = torch.full((F * n,), -1.0, dtype=torch.float32, device="cuda")
+    images = torch.full((F * W * H * 3,), -1.0, dtype=torch.float32, device="cuda")
+    st = ctx.render_views_device(cams, prm, W, H, 8, 0, 1, local.data_ptr(), None)
+    R.check(R.lib().rt_unpermute_views_device(W, H, 8, 1, F, R.C.c_void_p(local.data_ptr()),
+                                              R.C.c_void_p(images.data_ptr()), R.C.c_void_p(0)), "unpermute")
+    torch.cuda.synchronize()
+    imgs = images.view(F, H * W * 3)
+    rays = 0
+    for v, cam in enumerate(cams):
+        one, s1 = ctx.render(cam, prm, W, H)
+        rays += s1.rays
+        if v in (0, 21, 63):
+            assert imgs[v].cpu().numpy().tobytes() == one.tobytes(), v
+    assert st.rays == rays
+    view = imgs[21].cpu().numpy().reshape(H, W, 3)[::-1]  # [y][x], reference y order
+    lit = np.argwhere(view.max(axis=2) > 0)
+    pick = lit[np.random.default_rng(21).choice(len(lit), size=128, replace=False)][:, ::-1]
+    sel = np.random.default_rng(5).permutation(W * H)[:128]
+    xy = np.concatenate([np.stack([sel % W, sel // W], axis=1), pick]).astype(np.int32)
+    O.set_threads(_oracle_threads())
+    ref, _ = O.Oracle(scene).render_pixels(prm, W, H, xy, euler=eulers[21])
+    assert float(np.max(np.abs(view[xy[:, 1], xy[:, 0]] - ref))) <= TOL
