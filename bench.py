@@ -194,6 +194,7 @@ def main():
     gathered = (torch.zeros(b_count * local_buf.numel(), dtype=torch.float32, device=dev)
                 if rank == 0 or not to_root else None) if b_count > 1 else local_buf
     images = torch.zeros(F * W * H * 3, dtype=torch.float32, device=dev)
+    torch.cuda.synchronize(dev)  # the fills above ran on torch's default stream; the renders use bstream
 
     # one explicit stream for render, gather and un-permute (torch's default stream is the null
     # stream, which would let the un-permute of step k overlap the render of step k+1)

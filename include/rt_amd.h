@@ -27,7 +27,8 @@
  * int status: 0 = ok, < 0 = error (message via rt_last_error).  The caller owns every host
  * buffer it passes; a context owns its device memory.  Calls on one context must not be made
  * concurrently (the reference BVH is shared read-only by OpenMP threads; here the parallelism is
- * inside the GPU launch).  The *_device calls are asynchronous on the caller's stream unless
+ * inside the GPU launch).  The *_device calls are asynchronous on the caller's stream (NULL = the
+ * null stream, so they are ordered after the caller's default-stream work on their buffers) unless
  * `stats` is given; a context keeps ONE set of per-render scratch (camera table, job counters), so
  * its renders must be ordered on one stream (or separated by events) -- two renders of one
  * context in flight on different streams at once would share that scratch.

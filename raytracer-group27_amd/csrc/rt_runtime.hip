@@ -992,7 +992,7 @@ extern "C" int rt_render_device(rt_ctx* c, const rt_camera* cam, const rt_params
     K.n_local_bands = nbands > band_rank ? (nbands - band_rank + band_count - 1) / band_count : 0;
     K.view_rows = K.n_local_bands * band_rows;
     K.out = d_out;
-    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    hipStream_t st = (hipStream_t)stream;  // NULL: the null stream, ordered with the caller's default-stream work
     return launch_render(c, K, st, g_count_mode, stats);
 }
 
@@ -1036,7 +1036,7 @@ extern "C" int rt_render_views_device(rt_ctx* c, const rt_camera* cams, int n_vi
     }
     rc = ensure(c, &c->d_views, &c->views_bytes, v.size() * sizeof(float));
     if (rc != RT_OK) return rc;
-    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    hipStream_t st = (hipStream_t)stream;  // NULL: the null stream, ordered with the caller's default-stream work
     HIP_TRY(hipMemcpyAsync(c->d_views, v.data(), v.size() * sizeof(float), hipMemcpyHostToDevice, st));
     K.views = reinterpret_cast<const float*>(c->d_views);
     return launch_render(c, K, st, g_count_mode, stats);
