@@ -547,6 +547,17 @@ __device__ __attribute__((noinline)) bool advance_lights_call(const void* ka, La
     return advance_lights_body<TEX>(kernel_params(ka), L, have_result, vis, fan, q);
 }
 
+// ... the same with the lane state and query as PRIVATE-address-space references (they live in the
+// calling kernel's private frame): scratch instead of flat accesses.  Used where the state machine
+// is inline in the kernel (single-frame variants); inside the out-of-line advance it cost the batch
+// variant spilled registers (rejected list).
+#define RT_PRIV __attribute__((address_space(5)))
+template <bool TEX>
+__device__ __attribute__((noinline)) bool advance_lights_pcall(const void* ka, Lane RT_PRIV& L, bool have_result,
+                                                               bool vis, FanResult fan, Query RT_PRIV& q) {
+    return advance_lights_body<TEX>(kernel_params(ka), *(Lane*)&L, have_result, vis, fan, *(Query*)&q);
+}
+
 
 // ---- recursion tree ------------------------------------------------------------------------
 // Next lobe sample of the glossy frame f (src/main.cpp:209-249): two uniforms per draw from the
@@ -866,7 +877,7 @@ __device__ __attribute__((noinline)) int cansee_step_call(const void* ka, Query&
 // the cansee segment loop, the light loop, the recursion tree, the camera samples and the pixel
 // output.  Returns true with the next query in q (L.shadow says which kind); false when the lane's
 // job is complete (L.job = -1).
-template <bool COUNT, bool TEX>
+template <bool COUNT, bool TEX, bool PRIVL = false>
 __device__ __forceinline__ bool advance_lane(const KParams& P, const JobSrc& J, const void* ka, Lane& L, Frame* fr,
                                              bool hit, const Best& b, FanResult fan, Query& q, Cnt& cnt,
                                              uint32_t job_rays) {
@@ -883,7 +894,9 @@ __device__ __forceinline__ bool advance_lane(const KParams& P, const JobSrc& J, 
     bool more;
     if (L.shadow || hit) {
         L.shadow = false;
-        if (advance_lights_call<TEX>(ka, L, lights_have, lights_vis, fan, q)) return true;
+        if (PRIVL ? advance_lights_pcall<TEX>(ka, *(Lane RT_PRIV*)&L, lights_have, lights_vis, fan, *(Query RT_PRIV*)&q)
+                  : advance_lights_call<TEX>(ka, L, lights_have, lights_vis, fan, q))
+            return true;
         // every light done: the node's colour, then its mirror / reflected child
         L.acc = L.acc + L.w * L.color;
         if (L.desc) {
@@ -960,7 +973,7 @@ __device__ __forceinline__ bool advance_v(const KParams& P, const JobSrc& J, con
     if constexpr ((V & RT_V_CALL) != 0)
         return advance_lane_call<COUNT, TEX>(ka, L, fr, hit, b, fan, q, cnt, job_rays);
     else
-        return advance_lane<COUNT, TEX>(P, J, ka, L, fr, hit, b, fan, q, cnt, job_rays);
+        return advance_lane<COUNT, TEX, true>(P, J, ka, L, fr, hit, b, fan, q, cnt, job_rays);
 }
 
 // ---- whole-traversal persistent kernel ------------------------------------------------------
