@@ -107,11 +107,16 @@ def cpu_baseline(config, budget_s=12.0, seed=12345):
             "legs": legs}
 
 
-def load_pmc(config, kernel, sha):
+def pmc_key(config, views):
+    """The config key of a PMC summary (tools/pmc_summary.py's CONFIG argument): e.g. C3v64."""
+    return f"{config}v{views}"
+
+
+def load_pmc(config, kernel, sha, path=None):
     """HBM bytes per render launch from the committed rocprofv3 --pmc summary
     (profiles/pmc_latest.json, written by tools/pmc_summary.py --latest) -- used only when it was
     measured on this exact library build (sha) and kernel; returns (bytes or None, provenance)."""
-    p = os.path.join(REPO, "profiles", "pmc_latest.json")
+    p = path or os.path.join(REPO, "profiles", "pmc_latest.json")
     try:
         with open(p) as f:
             d = json.load(f)
@@ -276,7 +281,7 @@ def main():
         achieved = bytes0 / (avg_ms * 1e-3) / 1e9
         kname = st.kernel_name
         sha = lib_sha()
-        pmc, pmc_src = load_pmc(f"{args.config}v{F}", kname, sha)
+        pmc, pmc_src = load_pmc(pmc_key(args.config, F), kname, sha)
         line = {
             "metric": METRIC,
             "value": total_rays / max_elapsed / 1e6,
