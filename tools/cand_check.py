@@ -15,6 +15,10 @@ h = hashlib.sha256()
 for cfg in ("C3", "C2"):
     s, p, W, H, _ = R.build_config(cfg)
     ctx = R.Context(s)
+    if len(sys.argv) > 2:
+        for kv in sys.argv[2].split(","):
+            k, v = kv.split("=")
+            ctx.set_option(int(k), int(v))
     img, st = ctx.render(R.camera_from_trackball(aspect=R.aspect_of(W, H)), p, W, H)
     h.update(img.tobytes()); h.update(str(st.rays).encode())
     if cfg == "C3":
@@ -28,7 +32,8 @@ print(h.hexdigest())
 '''
 out = []
 for lib in (None, os.path.join(REPO, "raytracer-group27_amd", "build", "new_librt.so")):
-    r = subprocess.run([sys.executable, "-c", CODE] + ([lib] if lib else []), cwd=REPO, capture_output=True, text=True)
+    extra = [lib, os.environ["CAND_OPTS"]] if lib and os.environ.get("CAND_OPTS") else ([lib] if lib else [])
+    r = subprocess.run([sys.executable, "-c", CODE] + extra, cwd=REPO, capture_output=True, text=True)
     if r.returncode:
         print(r.stderr[-2000:])
         sys.exit(1)
