@@ -3,17 +3,21 @@
 Workload (config.workload): C3 = dragon proxy (800 000 triangles), 1920x1080,
 one point light, hard shadows + mirror recursion depth 4 (BASELINE.json configs[2]).  One step
 renders a batch of --views full frames (default 64: a turntable of the scene, 5.625 degrees apart) in
-ONE launch of the persistent kernel (rt_render_views_device), each frame un-permuted into its own
-Screen::m_textureData image.  Inputs (scene, BVH) are resident in HBM before timing starts.
+ONE launch of the persistent kernel (rt_render_views_image_device), every pixel stored straight into
+its frame's Screen::m_textureData image.  Inputs (scene, BVH) are resident in HBM before timing starts.
+--config C4 / C5 measure the other BASELINE configs the same way (C5: 3840x2160).
 
-N > 1 (one process per GPU, torch.distributed "nccl" = RCCL): the tile split of north_star.  Every
-rank renders its interleaved 8-row bands (band b -> rank b mod N) of ALL the step's views in one
-launch, the band buffers are gathered to rank 0 over xGMI (RCCL gather: every rank's buffer crosses
-its own link to rank 0, all links at once) and rank 0 un-permutes the views (one launch).  Per-step
-work is fixed as N grows ("scaling": "strong"), so N = 1 is exactly the BENCH workload.
---partition frames instead gives each rank its own turntable views (no collective on the data path).
+N > 1 (one process per GPU, torch.distributed "nccl" = RCCL for the control plane): the tile split of
+north_star.  Every rank renders its interleaved 8-row bands (band b -> rank b mod N) of ALL the step's
+views in one launch, storing each pixel straight into rank 0's images (allocated there and opened by the
+other ranks through an IPC handle: the pixel stores cross xGMI while the frame renders, so there is no
+gather step after it -- --exchange ipc, the default).  --exchange gather keeps the previous scheme
+(band buffers, RCCL gather to rank 0, one un-permute launch there) and is also the fallback when the
+IPC mapping fails.  Per-step work is fixed as N grows ("scaling": "strong"), so N = 1 is exactly the
+BENCH workload.  --partition frames instead gives each rank its own turntable views (no collective).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3] [--views V] [--no-cpu-baseline]
+                    [--exchange ipc|gather] [--cpu-pixels P] [--dump-images PATH]
 
 Prints ONE JSON line on rank 0.  `value` = rays (intersect() calls) of the step / max-rank time.
 """
@@ -66,11 +70,13 @@ def host_threads():
     return max(1, min(os.cpu_count() or 1, n if n > 0 else (os.cpu_count() or 1)))
 
 
-def cpu_baseline(config, budget_s=12.0, seed=12345):
+def cpu_baseline(config, budget_s=12.0, seed=12345, max_pixels=None):
     """The reference algorithm (oracle/ref_cpu.cpp, g++ -O2 -fopenmp) timed on the host: brute-force
     primary/secondary rays (useBVH=false, the reference default, src/main.cpp:60) and the reference's
     own depth-4 BVH (useBVH=true), each single-threaded and on every host core, on the first pixels
-    of BASELINE.md's seed-12345 permutation of the frame (rays counted exactly)."""
+    of BASELINE.md's seed-12345 permutation of the frame (rays counted exactly).  Each leg stops at
+    budget_s / 4 seconds or max_pixels pixels (BASELINE.md's sample: 4 096 for C3-C5, the whole frame for
+    C1/C2; tools/cpu_baseline.py runs those in full)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
     import rt_amd as R
@@ -78,6 +84,8 @@ def cpu_baseline(config, budget_s=12.0, seed=12345):
     scene, prm, W, H, _ = R.build_config(config)
     orc = O.Oracle(scene)
     order = np.random.default_rng(seed).permutation(W * H)
+    if max_pixels:
+        order = order[:max_pixels]
     allc = host_threads()
     legs = {}
     for bvh in (0, 1):
@@ -148,6 +156,14 @@ def main():
                     help="frames per step, rendered in ONE launch (rt_render_views_device)")
     ap.add_argument("--view-step", type=float, default=None,
                     help="turntable step between views in degrees (default 360 / views)")
+    ap.add_argument("--exchange", choices=("ipc", "gather"), default="ipc",
+                    help="N>1 bands: ipc = every rank stores its pixels straight into rank 0's images (IPC-mapped, "
+                         "no gather step); gather = band buffers + RCCL gather + un-permute on rank 0")
+    ap.add_argument("--cpu-pixels", type=int, default=0,
+                    help="CPU baseline: stop each leg at this many pixels as well as at --cpu-budget (0: budget only)")
+    ap.add_argument("--resolution", default=None, help="WxH override (tests; the BENCH line uses the config's)")
+    ap.add_argument("--dragon-uv", default=None, help="UxV dragon-proxy tessellation override (tests)")
+    ap.add_argument("--dump-images", default=None, help="rank 0 saves the last step's images (.npy; tests)")
     args = ap.parse_args()
 
     import torch
@@ -170,7 +186,10 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    scene, prm, W, H, desc = R.build_config(args.config)
+    uv = tuple(int(x) for x in args.dragon_uv.split("x")) if args.dragon_uv else None
+    scene, prm, W, H, desc = R.build_config(args.config, dragon_uv=uv)
+    if args.resolution:
+        W, H = (int(x) for x in args.resolution.split("x"))
     F = max(1, args.views)
     bands = args.partition == "bands"
     b_rank, b_count = (rank, world) if bands else (0, 1)
@@ -190,31 +209,59 @@ def main():
     upload_s = time.perf_counter() - t_up
     build_info = ctx.build_info()
 
+    img_elems = F * W * H * 3
+    exchange = "local" if (world == 1 or not bands) else args.exchange
+    ipc = None
+    if exchange == "ipc":
+        # rank 0's images, opened by every other rank: the ranks' kernels store their pixels into them
+        try:
+            if rank == 0:
+                ipc = R.IpcBuffer(local, nbytes=img_elems * 4)
+            obj = [ipc.handle if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            if rank != 0:
+                ipc = R.IpcBuffer(local, handle=obj[0])
+            ok = 1
+        except R.RtError as e:  # no IPC on this node: the gather scheme
+            print(f"rank {rank}: IPC mapping failed ({e}); falling back to --exchange gather", file=sys.stderr)
+            ok = 0
+        flag = torch.tensor([ok], dtype=torch.int32, device=dev if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if not int(flag.item()):
+            if ipc is not None:
+                ipc.close()
+            ipc = None
+            exchange = "gather"
+    images = None if exchange == "ipc" else torch.zeros(img_elems, dtype=torch.float32, device=dev)
+    img_ptr = ipc.ptr if exchange == "ipc" else images.data_ptr()
     nbands = (H + BAND_ROWS - 1) // BAND_ROWS
     max_local = (nbands + b_count - 1) // b_count
-    view_elems = max_local * BAND_ROWS * W * 3
-    local_buf = torch.zeros(F * view_elems, dtype=torch.float32, device=dev)
-    # RCCL: gather to rank 0; the gloo rehearsal (BENCH_DIST_BACKEND=gloo, device tensors) all-gathers instead
-    to_root = world > 1 and dist.get_backend() == "nccl"
-    gathered = (torch.zeros(b_count * local_buf.numel(), dtype=torch.float32, device=dev)
-                if rank == 0 or not to_root else None) if b_count > 1 else local_buf
-    images = torch.zeros(F * W * H * 3, dtype=torch.float32, device=dev)
+    if exchange == "gather":
+        view_elems = max_local * BAND_ROWS * W * 3
+        local_buf = torch.zeros(F * view_elems, dtype=torch.float32, device=dev)
+        # RCCL: gather to rank 0; the gloo rehearsal (BENCH_DIST_BACKEND=gloo, device tensors) all-gathers instead
+        to_root = dist.get_backend() == "nccl"
+        gathered = (torch.zeros(b_count * local_buf.numel(), dtype=torch.float32, device=dev)
+                    if rank == 0 or not to_root else None)
     torch.cuda.synchronize(dev)  # the fills above ran on torch's default stream; the renders use bstream
 
-    # one explicit stream for render, gather and un-permute (torch's default stream is the null
-    # stream, which would let the un-permute of step k overlap the render of step k+1)
+    # one explicit stream for the step's work (torch's default stream is the null stream)
     bstream = torch.cuda.Stream(dev)
 
-    def step():
+    def step(cams_=cams):
         with torch.cuda.stream(bstream):
-            st = ctx.render_views_device(cams, prm, W, H, BAND_ROWS, b_rank, b_count, local_buf.data_ptr(),
+            if exchange != "gather":  # each pixel straight into its image (rank 0's, IPC-mapped, for N > 1)
+                return ctx.render_views_image_device(cams_, prm, W, H, img_ptr, bstream.cuda_stream, band_rank=b_rank,
+                                                     band_count=b_count)
+            st = ctx.render_views_device(cams_, prm, W, H, BAND_ROWS, b_rank, b_count, local_buf.data_ptr(),
                                          bstream.cuda_stream)
-            if b_count > 1 and to_root:  # to rank 0 only: each rank's bands cross one xGMI link, all at once
+            if to_root:  # to rank 0 only: each rank's bands cross one xGMI link, all at once
                 dist.gather(local_buf, gather_list=list(gathered.chunk(b_count)) if rank == 0 else None, dst=0)
-            elif b_count > 1:
+            else:
                 dist.all_gather_into_tensor(gathered, local_buf)
-            if rank == 0 or not bands:
-                R.check(R.lib().rt_unpermute_views_device(W, H, BAND_ROWS, b_count, F, R.C.c_void_p(gathered.data_ptr()),
+            if rank == 0:
+                R.check(R.lib().rt_unpermute_views_device(W, H, BAND_ROWS, b_count, len(cams_),
+                                                          R.C.c_void_p(gathered.data_ptr()),
                                                           R.C.c_void_p(images.data_ptr()),
                                                           R.C.c_void_p(bstream.cuda_stream)), "unpermute")
         return st
@@ -247,20 +294,36 @@ def main():
     # single-frame latency beside the batch: the default view alone (this rank's bands), one launch
     single = None
     if F > 1 and not args.no_single_frame:
-        one_cam = R.camera_from_trackball(aspect=R.aspect_of(W, H))
-        one = ctx.render_device(one_cam, prm, W, H, BAND_ROWS, b_rank, b_count, local_buf.data_ptr(), None)
+        one_cam = [R.camera_from_trackball(aspect=R.aspect_of(W, H))]
+
+        def frame():
+            if exchange != "gather":  # into view 0 of the images (rank 0's for N > 1)
+                return step(one_cam)
+            # gather scheme: the rank's bands of the frame alone (per-GPU latency, no gather)
+            return ctx.render_device(one_cam[0], prm, W, H, BAND_ROWS, b_rank, b_count, local_buf.data_ptr(), None)
+
+        one = frame()
         n1 = max(5, args.steps)
         barrier()
         t1 = time.perf_counter()
         r1, k1 = 0, []
         for _ in range(n1):
-            one = ctx.render_device(one_cam, prm, W, H, BAND_ROWS, b_rank, b_count, local_buf.data_ptr(), None)
+            one = frame()
             r1 += one.rays
             k1.append(one.kernel_ms)
         barrier()
         e1 = time.perf_counter() - t1
         single = {"ms_per_frame": e1 / n1 * 1e3, "kernel_ms": float(np.mean(k1)), "rays_per_frame": int(one.rays),
                   "Mrays_per_s_per_gpu": r1 / e1 / 1e6, "frames": n1, "kernel": one.kernel_name}
+        step()  # the last step's images again (--dump-images)
+        barrier()
+
+    if args.dump_images and rank == 0:
+        if exchange == "ipc":
+            out = R.device_to_host(img_ptr, img_elems)
+        else:
+            out = images.cpu().numpy()
+        np.save(args.dump_images, out.reshape(F, -1))
 
     t = torch.tensor([elapsed, float(rays), float(np.mean(kms)), float(cst.node_visits), float(cst.tri_tests),
                       float(cst.hits), float(cst.rays)], dtype=torch.float64, device=dev)
@@ -301,9 +364,13 @@ def main():
                        "rays_per_frame": int(total_rays / args.steps / (1 if bands else world) / F),
                        "band_rows": BAND_ROWS,
                        "partition": (f"{world}-GPU tile split: interleaved 8-row bands of every view, "
-                                     + ("RCCL gather to rank 0" if to_root else f"{dist.get_backend()} all-gather")
+                                     + ("each rank's pixels stored straight into rank 0's images (IPC-mapped, "
+                                        "stores over xGMI while rendering; no gather step)" if exchange == "ipc" else
+                                        "RCCL gather to rank 0 + un-permute" if to_root else
+                                        f"{dist.get_backend()} all-gather + un-permute")
                                      if bands and world > 1 else
-                                     f"{world} GPU(s), {F} whole frame(s) per GPU per step"),
+                                     f"{world} GPU(s), {F} whole frame(s) per GPU per step, pixels stored in "
+                                     "their images (setPixel layout)"),
                        "scene_upload_s": round(upload_s, 4),
                        "scene_upload_first_s": round(upload_cold_s, 3),
                        "scene_build": "GPU (rt_build.hip)" if build_info["gpu"] else "host (bvh_build.cpp)",
@@ -321,8 +388,14 @@ def main():
         if single is not None:
             line["single_frame"] = single
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(args.config, budget_s=args.cpu_budget)
+            line["cpu_baseline"] = cpu_baseline(args.config, budget_s=args.cpu_budget, max_pixels=args.cpu_pixels or None)
         print(json.dumps(line), flush=True)
+    if ipc is not None and not ipc.owner:  # the importers unmap rank 0's images before rank 0 frees them
+        ipc.close()
+    if world > 1:
+        dist.barrier()
+    if ipc is not None:
+        ipc.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

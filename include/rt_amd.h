@@ -5,13 +5,17 @@
  * (catalinlup/RayTracer-Group27, paths relative to the reference root):
  *
  *   rt_create            BoundingVolumeHierarchy::BoundingVolumeHierarchy(Scene*)
- *                        src/bounding_volume_hierarchy.h:24, .cpp:5-9 (+ scene upload)
+ *                        src/bounding_volume_hierarchy.h:24, .cpp:5-9 (+ scene upload), over a device list:
+ *                        one scene replica per GPU
  *   rt_intersect         bool BoundingVolumeHierarchy::intersect(Ray&, HitInfo&, bool useBVH) const
  *                        src/bounding_volume_hierarchy.h:33, .cpp:49-78
  *   rt_shade             static glm::vec3 getFinalColor(Scene&, const BVH&, Ray, int level=0)
  *                        src/main.cpp:129-301
  *   rt_render            static void renderRayTracing(Scene&, const Trackball&, const BVH&, Screen&, ...)
  *                        src/main.cpp:340-400 (+ Screen::setPixel src/screen.cpp:32-38)
+ *   rt_render_views_image_device  renderRayTracing's pixel loop split over the context's GPUs (the OpenMP
+ *                        row split, src/main.cpp:344-347): every GPU stores its bands straight into
+ *                        the setPixel layout on the first GPU -- no gather, no un-permute
  *   rt_render_device     same as rt_render, band-partitioned, device-resident output (multi-GPU path)
  *   rt_render_views_device  a batch of rt_render_device frames (one camera each) in one launch
  *   rt_render_views      the same batch, host output in the rt_render layout
@@ -32,6 +36,19 @@
  * `stats` is given; a context keeps ONE set of per-render scratch (camera table, job counters), so
  * its renders must be ordered on one stream (or separated by events) -- two renders of one
  * context in flight on different streams at once would share that scratch.
+ *
+ * Multi-device contexts (rt_create with ndev > 1): devices[0] is the context's home device; its
+ * streams (the caller's, for the *_device calls) order every call.  rt_render, rt_render_views and
+ * rt_render_views_image_device split the frame's interleaved 8-row bands over every device (one host
+ * thread per extra device); each extra device waits for the caller stream's earlier work and the
+ * caller stream waits for it before its later work, so the call keeps single-stream semantics.  The
+ * per-ray and band-dense calls (rt_intersect, rt_shade, rt_render_device, rt_render_views_device,
+ * rt_texture_sample) run on devices[0] alone.  A device may appear more than once (replicas on one
+ * GPU: the parity tests' stand-in for a multi-GPU node).
+ *
+ * Edits (rt_update_lights, rt_update_materials) first wait for every render in flight on every device
+ * of the context (device-wide synchronise), then replace the arrays: renders enqueued after the edit
+ * returns see the new values, none sees a mix.
  */
 #ifndef RT_AMD_H
 #define RT_AMD_H
@@ -43,8 +60,10 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 4  /* 2: textures; 3: rt_render_views_device; 4: rt_stats.ub_hits / .kernel,
-                             rt_ctx_set_option, rt_update_lights / _materials, rt_texture_sample */
+#define RT_ABI_VERSION 5  /* 2: textures; 3: rt_render_views_device; 4: rt_stats.ub_hits / .kernel,
+                             rt_ctx_set_option, rt_update_lights / _materials, rt_texture_sample;
+                             5: rt_create over a device list, rt_render_views_image_device, rt_ipc_*,
+                             rt_ctx_devices */
 
 /* status codes */
 #define RT_OK 0
@@ -253,10 +272,15 @@ int rt_camera_from_trackball(const float look_at[3], const float euler_radians[3
  * torch initialise the GPU before this library is loaded (rt_amd.py does; the other order leaves
  * one of the two runtimes without a device). */
 int rt_device_count(int* n);
-int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out);
+/* BoundingVolumeHierarchy(Scene*) over devices[0..ndev): a whole scene replica (acceleration structures
+ * built on that device) per entry, peer access from every other device to devices[0]. */
+int rt_create(const rt_scene_desc* desc, const int* devices, int ndev, rt_ctx** out);
+/* The context's device list into out (up to n entries); returns ndev. */
+int rt_ctx_devices(rt_ctx* ctx, int* out, int n);
 int rt_destroy(rt_ctx* ctx);
 
-/* Whole frame to host memory: rgb_out = W*H*3 floats in Screen::m_textureData order. */
+/* Whole frame to host memory: rgb_out = W*H*3 floats in Screen::m_textureData order (every device of
+ * the context renders its bands). */
 int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_params* params, int width, int height,
               float* rgb_out, rt_stats* stats);
 
@@ -286,9 +310,22 @@ int rt_render_views_device(rt_ctx* ctx, const rt_camera* cams, int n_views, cons
                            float* d_rgb_out, void* stream, rt_stats* stats);
 /* View batch to host memory: rgb_out = n_views frames of W*H*3 floats, each in Screen::m_textureData
  * order (the rt_render layout), view v at v*W*H*3.  Same kernel and results as
- * rt_render_views_device; stats summed over the views. */
+ * rt_render_views_device; stats summed over the views (and devices). */
 int rt_render_views(rt_ctx* ctx, const rt_camera* cams, int n_views, const rt_params* params, int width,
                     int height, float* rgb_out, rt_stats* stats);
+/*
+ * The frames' pixels straight into their final place: view v's pixel (x, y) at
+ * d_images[v*W*H*3 + ((H-1-y)*W + x)*3] (Screen::setPixel, src/screen.cpp:32-38).  Renders the bands
+ * b % band_count == band_rank (0, 1: the whole frame) split further over the context's devices
+ * (b / band_count % ndev picks the device).  d_images is device memory of devices[0] -- or of another
+ * process's GPU opened with rt_ipc_open (one process per GPU: each rank passes its own band_rank and
+ * rank 0's images, and the exchange is the kernels' pixel stores over xGMI).  Asynchronous on the
+ * caller's stream unless stats is given; bit-identical to rt_render_views.
+ */
+int rt_render_views_image_device(rt_ctx* ctx, const rt_camera* cams, int n_views, const rt_params* params, int width,
+                                 int height, int band_rows, int band_rank, int band_count, float* d_images,
+                                 void* stream, rt_stats* stats);
+
 /* Un-permute gathered band buffers ([band_count][max_local_bands][band_rows][W][3]) into the
  * setPixel layout on the device. */
 int rt_unpermute_bands_device(int width, int height, int band_rows, int band_count,
@@ -368,6 +405,20 @@ int rt_selftest_math(rt_ctx* ctx, const float* x, const float* y, int n, float* 
 /* Philox-4x32-10 (the glossy-lobe stream that replaces rand(), src/main.cpp:234-235): the same
  * host/device function the kernels call, exported for known-answer tests. */
 int rt_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+
+/* ---- device memory shared between processes (one process per GPU) --------------------------------
+ * rt_ipc_alloc: hipMalloc on `device` + its IPC handle (RT_IPC_HANDLE_BYTES bytes) for other processes;
+ * rt_ipc_open: map another process's buffer into this one (peer access from `device`); rt_ipc_close
+ * unmaps it; rt_device_free frees an rt_ipc_alloc buffer; rt_device_synchronize waits for every
+ * stream of a device. */
+#define RT_IPC_HANDLE_BYTES 64
+int rt_ipc_alloc(int device, size_t bytes, void** d_ptr, uint8_t handle[RT_IPC_HANDLE_BYTES]);
+int rt_ipc_open(int device, const uint8_t handle[RT_IPC_HANDLE_BYTES], void** d_ptr);
+int rt_ipc_close(void* d_ptr);
+int rt_device_free(int device, void* d_ptr);
+int rt_device_synchronize(int device);
+/* Synchronous copy of `bytes` from device memory (this library's, e.g. an rt_ipc_alloc buffer) to host. */
+int rt_memcpy_dtoh(void* host, const void* d_ptr, size_t bytes);
 
 /* ---- Screen post-processing (src/screen.cpp) ------------------------------------------------
  * Settings of class Screen (src/screen.h:58-111), raw values as the GUI passes them to the

@@ -328,7 +328,14 @@ class BoundingVolumeHierarchy {
 public:
     // Flattens the scene mesh-major exactly as loadObjectsFromScene does
     // (src/bounding_volume_hierarchy.cpp:80-99) and uploads it once.
-    explicit BoundingVolumeHierarchy(Scene* pScene, int device = 0) : scene_(pScene) {
+    // Every visible GPU by default (renderRayTracing splits the frame's bands over them, as the reference's
+    // OpenMP row loop uses every core), or the given device list.
+    explicit BoundingVolumeHierarchy(Scene* pScene, std::vector<int> devices = {}) : scene_(pScene) {
+        if (devices.empty()) {
+            int n = 0;
+            check(rt_device_count(&n), "BoundingVolumeHierarchy");
+            for (int i = 0; i < n; ++i) devices.push_back(i);
+        }
         const Scene& sc = *pScene;
         size_t ntri = 0;
         for (const Mesh& m : sc.meshes) ntri += m.triangles.size();
@@ -385,7 +392,7 @@ public:
         d.num_textures = (int)texs.size();
         d.textures = texs.data();
         lights_of(sc, d);
-        check(rt_create(&d, device, &ctx_), "BoundingVolumeHierarchy");
+        check(rt_create(&d, devices.data(), (int)devices.size(), &ctx_), "BoundingVolumeHierarchy");
         mesh_tex_.clear();
         for (const rt_material& m : mats) mesh_tex_.push_back(m.texture);
         synced_mats_ = mats;

@@ -12,6 +12,8 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "build", "liboracle.so")
+if os.environ.get("ORACLE_SANITIZER_LIB"):  # tools/sanitize/run.sh: the ASan/UBSan build of the same sources
+    LIB = os.environ["ORACLE_SANITIZER_LIB"]
 
 _lib = None
 

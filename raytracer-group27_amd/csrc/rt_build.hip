@@ -400,7 +400,7 @@ struct Ctrs {
 // the SAH decision of Bvh2Builder::build for bins that hold the whole range (n > kSmall > 2 * max_leaf:
 // a split is always taken); children: leaf descriptors, subtree tasks or next-level tasks
 __global__ void k_split(const LTask* __restrict__ tasks, int ntask, const uint32_t* __restrict__ bins, Split* splits,
-                        Bvh2Node* nodes, LTask* next, STask* small, Ctrs* ctr) {
+                        Bvh2Node* nodes, LTask* next, int cap_next, STask* small, int cap_small, Ctrs* ctr) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= ntask) return;
     const LTask T = tasks[t];
@@ -491,7 +491,11 @@ __global__ void k_split(const LTask* __restrict__ tasks, int ntask, const uint32
                 c.clo[a] = cclo[a];
                 c.chi[a] = cchi[a];
             }
-            next[atomicAdd(&ctr->nlarge, 1)] = c;
+            // capacities hold by construction (disjoint ranges of > kSmall / > kMaxLeaf triangles); an
+            // overflow is reported (host fallback) instead of written past the buffer
+            const int slot = atomicAdd(&ctr->nlarge, 1);
+            if (slot < cap_next) next[slot] = c;
+            else ctr->error = 1;
         } else {
             STask c;
             c.begin = cb[k];
@@ -505,7 +509,9 @@ __global__ void k_split(const LTask* __restrict__ tasks, int ntask, const uint32
                 c.clo[a] = cclo[a];
                 c.chi[a] = cchi[a];
             }
-            small[atomicAdd(&ctr->nsmall, 1)] = c;
+            const int slot = atomicAdd(&ctr->nsmall, 1);
+            if (slot < cap_small) small[slot] = c;
+            else ctr->error = 1;
         }
     }
     nodes[T.node] = nd;
@@ -1314,7 +1320,8 @@ bool gpu_build(const float* h_pos, int ntri, const float* sph4, int nsph, GpuBui
         GB_CHECK(hipMemsetAsync(&ctr->nlarge, 0, sizeof(int), st));
         k_init_bins<<<grid((long long)nlevel * NB * kBinW, 256), 256, 0, st>>>(bins, nlevel);
         k_bin<<<nc, 256, 0, st>>>(d_chunks, lt, idx, bmin, bmax, cent, bins);
-        k_split<<<grid(nlevel, 64), 64, 0, st>>>(lt, nlevel, bins, splits, nodes2, lt_next, small, ctr);
+        k_split<<<grid(nlevel, 64), 64, 0, st>>>(lt, nlevel, bins, splits, nodes2, lt_next, max_tasks, small, max_small,
+                                                 ctr);
         k_part_count<<<nc, 256, 0, st>>>(d_chunks, splits, idx, cent, nleft);
         k_part_scan<<<1, 1, 0, st>>>(d_chunks, nc, nleft);
         k_part_scatter<<<nc, 256, 0, st>>>(d_chunks, lt, splits, nleft, idx, cent, idx2);
@@ -1338,6 +1345,10 @@ bool gpu_build(const float* h_pos, int ntri, const float* sph4, int nsph, GpuBui
     GB_CHECK(hipMemcpyAsync(&hc, ctr, sizeof(Ctrs), hipMemcpyDeviceToHost, st));
     GB_CHECK(hipStreamSynchronize(st));
     TRACE("bvh2 levels");
+    if (hc.error || hc.nsmall > max_small) {
+        err = "GPU build: subtree task list overflow";
+        return false;
+    }
     if (hc.nsmall > 0) k_subtrees<<<grid(hc.nsmall, 4), 256, 0, st>>>(small, hc.nsmall, idx, idx2, bmin, bmax, cent,
                                                                       nodes2, ctr);
     GB_CHECK(hipGetLastError());
@@ -1409,7 +1420,8 @@ bool gpu_build(const float* h_pos, int ntri, const float* sph4, int nsph, GpuBui
     }
 
     out.ms[2] = ms_now();  // + BVH8
-    // ---- 4. records; outputs in exact-size buffers the context owns ----
+    // ---- 4. records; outputs in exact-size buffers the context owns (handed over only on success:
+    // every failure path below frees them) ----
     float4* rec = nullptr;
     float4* n8 = nullptr;
     GB_CHECK(hipMalloc(&rec, (size_t)ntri * 64));
@@ -1418,12 +1430,18 @@ bool gpu_build(const float* h_pos, int ntri, const float* sph4, int nsph, GpuBui
         err = "GPU build: out of device memory";
         return false;
     }
+    k_records<<<grid(ntri, 256), 256, 0, st>>>(order8, ntri, pos, tri_key, tri_leaf, rec);
+    hipError_t e = hipMemcpyAsync(n8, nodes8, (size_t)nodes_total * 128, hipMemcpyDeviceToDevice, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e == hipSuccess) e = hipGetLastError();
+    if (e != hipSuccess) {
+        hipFree(rec);
+        hipFree(n8);
+        err = std::string("GPU build: ") + hipGetErrorString(e) + " (records)";
+        return false;
+    }
     out.tri = rec;
     out.nodes = n8;
-    k_records<<<grid(ntri, 256), 256, 0, st>>>(order8, ntri, pos, tri_key, tri_leaf, rec);
-    GB_CHECK(hipMemcpyAsync(n8, nodes8, (size_t)nodes_total * 128, hipMemcpyDeviceToDevice, st));
-    GB_CHECK(hipStreamSynchronize(st));
-    GB_CHECK(hipGetLastError());
     out.ms[3] = ms_now();  // + records
     out.nnodes = nodes_total;
     out.max_depth = depth8;

@@ -96,6 +96,8 @@ struct KParams {
     // bands
     int band_rows, band_rank, band_count, n_local_bands;
     float* out;
+    int out_image;              // 0: band-dense rows (rt_render_device); 1: Screen::m_textureData order, view v's
+                                // image at out + v * W * H * 3 (setPixel's row H-1-y, src/screen.cpp:32-38)
     unsigned long long* stats;  // rays, node visits, tri tests, hits, ..., UB-regime hits
     int refill;                 // dynamic-fetch kernel: waiting lanes that end a traversal phase
     int shade_level;            // rt_shade: recursion level of the explicit rays (getFinalColor's `level`)

@@ -793,7 +793,7 @@ __device__ __forceinline__ void queue_camera(const KParams& P, Lane& L, Query& q
 }
 
 // Map a job index to its pixel (8x8 tiles inside the rank's bands): the reference's pixel id and the
-// pixel's row in the band buffer.  False if outside the image.
+// pixel's row in the output (band buffer or final image).  False if outside the image.
 __device__ __forceinline__ bool job_pixel(const KParams& P, int gjob, uint32_t& rpix, int& out_row) {
     int view;
     int job = view_job(P, gjob, view);
@@ -817,7 +817,9 @@ __device__ __forceinline__ bool job_pixel(const KParams& P, int gjob, uint32_t& 
     const int px = tx * 8 + (lane & 7);
     const int py = gb * P.band_rows + row_in_band;
     rpix = (uint32_t)(py * P.W + px);  // the reference's pixel (x, y), y up
-    out_row = view * P.view_rows + lb * P.band_rows + row_in_band;
+    // band-dense rows of this rank, or the pixel's final row (setPixel: row H-1-y of view v's image,
+    // src/screen.cpp:32-38) in the caller's images -- local HBM or another device's, peer-mapped
+    out_row = P.out_image ? view * P.H + (P.H - 1 - py) : view * P.view_rows + lb * P.band_rows + row_in_band;
     return (px < P.W) && (row_in_band < P.band_rows) && (py < P.H) && (lb < P.n_local_bands);
 }
 

@@ -11,10 +11,15 @@
 #include <chrono>
 #include <cfloat>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/rt_amd.h"
@@ -35,14 +40,61 @@ using namespace rt;
 #define RT_GPU_BUILD_MIN 65536
 static int g_build_mode = 0;  // rt_set_build_mode: 0 by size, 1 host, 2 GPU
 
+// One host thread per extra device of a multi-device context: it creates that device's
+// scene replica and enqueues that device's part of every split render, so the devices' host work
+// (argument setup, launches, the stats read-back) runs side by side.  post() hands over one task,
+// wait() returns once it has run.
+class DeviceWorker {
+public:
+    DeviceWorker() : th_([this] { loop(); }) {}
+    ~DeviceWorker() {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        th_.join();
+    }
+    void post(std::function<void()> f) {
+        std::lock_guard<std::mutex> lk(m_);
+        task_ = std::move(f);
+        has_ = true;
+        done_ = false;
+        cv_.notify_all();
+    }
+    void wait() {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [&] { return done_; });
+    }
+
+private:
+    void loop() {
+        std::unique_lock<std::mutex> lk(m_);
+        for (;;) {
+            cv_.wait(lk, [&] { return stop_ || has_; });
+            if (!has_) return;  // stop
+            std::function<void()> f = std::move(task_);
+            has_ = false;
+            lk.unlock();
+            f();
+            lk.lock();
+            done_ = true;
+            cv_.notify_all();
+        }
+    }
+    std::mutex m_;
+    std::condition_variable cv_;
+    std::function<void()> task_;
+    bool has_ = false, done_ = true, stop_ = false;
+    std::thread th_;  // last: starts once the members above exist
+};
+
 struct rt_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     DevScene S{};  // quantised BVH8 nodes + triangle records in its leaf order, shading data, lights
     std::vector<void*> allocs;
     unsigned long long* d_stats = nullptr;
-    float* d_fb = nullptr;
-    size_t fb_bytes = 0;
     float* d_img = nullptr;
     size_t img_bytes = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -76,6 +128,20 @@ struct rt_ctx {
     int opt_dual = -1;        // dynamic-fetch steps: record and node visit in one iteration (-1 default, 0 off, 1 on)
     int opt_variant = -1;   // -1: the shipped variant for the render shape (RT_DF_BATCH / _FRAME, RT_WT_DEFAULT)
     char last_kernel[64] = {0};
+    // view batches: the camera table's pinned host staging and the event of its last copy (the buffer
+    // is refilled only once that copy has read it)
+    float* h_views = nullptr;
+    size_t h_views_bytes = 0;
+    hipEvent_t ev_views = nullptr;
+    // multi-device context (rt_create over a device list): replicas[0] is this context on devices[0],
+    // replicas[i] a whole scene replica on devices[i] driven by workers[i]; a split render gives
+    // replica i every band b with b % n == i (of the caller's bands) and lands its pixels straight in
+    // the caller's images on devices[0] (peer access)
+    std::vector<int> devices;
+    std::vector<rt_ctx*> replicas;
+    std::vector<std::unique_ptr<DeviceWorker>> workers;
+    hipEvent_t ev_ready = nullptr;  // devices[0]: the caller stream's work before a split render
+    hipEvent_t ev_done = nullptr;   // this replica's part of the last split render
 };
 
 // Image::Image + initMipmap (src/image.cpp:37-73,408-452): texel k = rgb[k*channels + 0..2] / 255.0f
@@ -163,12 +229,18 @@ static int ensure(rt_ctx* c, float** buf, size_t* cap, size_t bytes) {
 
 extern "C" int rt_destroy(rt_ctx* c) {
     if (!c) return RT_OK;
+    c->workers.clear();  // joins the device threads
+    for (size_t i = 1; i < c->replicas.size(); ++i) rt_destroy(c->replicas[i]);
+    c->replicas.clear();
     hipSetDevice(c->device);
+    if (c->ev_ready) hipEventDestroy(c->ev_ready);
+    if (c->ev_done) hipEventDestroy(c->ev_done);
+    if (c->ev_views) hipEventDestroy(c->ev_views);
+    if (c->h_views) hipHostFree(c->h_views);
     for (void* p : c->allocs) hipFree(p);
     for (void* p : c->d_lights)
         if (p) hipFree(p);
     if (c->d_stats) hipFree(c->d_stats);
-    if (c->d_fb) hipFree(c->d_fb);
     if (c->d_img) hipFree(c->d_img);
     if (c->ev0) hipEventDestroy(c->ev0);
     if (c->ev1) hipEventDestroy(c->ev1);
@@ -196,7 +268,8 @@ extern "C" int rt_device_count(int* n) {
     const hipError_t e = hipGetDeviceCount(n);
     if (e != hipSuccess) {
         *n = 0;
-        set_error(std::string("rt_device_count: ") + hipGetErrorString(e));
+        set_error(std::string("rt_device_count: no HIP device available (the MI355X path has no CPU fallback): ") +
+                  hipGetErrorString(e));
         return RT_ERR_NO_DEVICE;
     }
     return RT_OK;
@@ -272,24 +345,11 @@ static double ms_since(std::chrono::steady_clock::time_point t0) {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
-extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
+// One scene replica on one device: the acceleration structures (GPU or host build), the uploads, the
+// per-render scratch.  rt_create makes one per entry of its device list.
+static int create_one(const rt_scene_desc* desc, int device, rt_ctx** out) {
     const auto t_start = std::chrono::steady_clock::now();
-    if (!desc || !out) {
-        set_error("rt_create: null argument");
-        return RT_ERR_INVALID;
-    }
     *out = nullptr;
-    int ndev = 0;
-    const hipError_t de = hipGetDeviceCount(&ndev);
-    if (de != hipSuccess || ndev == 0) {
-        set_error(std::string("rt_create: no HIP device available (the MI355X path has no CPU fallback): ") +
-                  (de != hipSuccess ? hipGetErrorString(de) : "0 devices"));
-        return RT_ERR_NO_DEVICE;
-    }
-    if (device < 0 || device >= ndev) {
-        set_error("rt_create: device index out of range");
-        return RT_ERR_INVALID;
-    }
     const int ntri = desc->num_triangles;
     if (ntri < 0 || (ntri > 0 && (!desc->positions || !desc->normals || !desc->mesh_index)) ||
         desc->num_meshes < 0 || (ntri > 0 && !desc->materials) || desc->num_spheres < 0 ||
@@ -328,9 +388,13 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
         std::string gerr;
         t_gpu = ms_since(t_start);
         gpu_built = gpu_build(desc->positions, ntri, sph4.data(), desc->num_spheres, gbuild, gerr);
+        if (gpu_built) {  // the context owns the built records and nodes from here on (every exit frees them)
+            c->allocs.push_back(gbuild.tri);
+            c->allocs.push_back(gbuild.nodes);
+        }
         if (!gpu_built && g_build_mode == 2) {
             set_error("rt_create: " + gerr);
-            delete c;
+            rt_destroy(c);
             return RT_ERR_INVALID;
         }
     }
@@ -340,7 +404,7 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
         else ref = build_ref_bvh(desc->positions, ntri, sph4.data(), desc->num_spheres, 4);
     } catch (const std::exception& ex) {
         set_error(std::string("rt_create: ") + ex.what());
-        delete c;
+        rt_destroy(c);
         return RT_ERR_INVALID;
     }
     c->create_ms[1] = gpu_built ? t_gpu + gbuild.ms[0] : ms_since(t_start);  // + reference BVH
@@ -348,7 +412,7 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
     c->ref_levels = ref.max_level_achieved + 1;
     if (c->ref_nodes > RT_MAX_REF_NODES) {
         set_error("rt_create: reference BVH larger than 31 nodes");
-        delete c;
+        rt_destroy(c);
         return RT_ERR_INVALID;
     }
     std::vector<DRefNode> refn(ref.nodes.size());
@@ -379,8 +443,6 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
     const float eps = std::ldexp(max_abs, -16);
     Bvh8 bvh8;
     if (gpu_built) {
-        c->allocs.push_back(gbuild.tri);
-        c->allocs.push_back(gbuild.nodes);
         c->S.tri = static_cast<const float4*>(gbuild.tri);
         c->S.nodes = static_cast<const float4*>(gbuild.nodes);
         bvh8.max_depth = gbuild.max_depth;
@@ -395,7 +457,7 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
             c->bvh2_depth = bvh.max_depth;
         } catch (const std::exception& ex) {
             set_error(std::string("rt_create: ") + ex.what());
-            delete c;
+            rt_destroy(c);
             return RT_ERR_INVALID;
         }
     }
@@ -518,6 +580,105 @@ extern "C" int rt_create(const rt_scene_desc* desc, int device, rt_ctx** out) {
     return RT_OK;
 }
 
+static std::string last_error_text() {
+    char buf[1024] = {0};
+    rt_last_error(buf, sizeof(buf));
+    return buf;
+}
+
+// BoundingVolumeHierarchy(Scene*) (src/bounding_volume_hierarchy.h:24) over a device list:
+// a whole scene replica per device (the OpenMP threads of renderRayTracing share one read-only BVH,
+// src/main.cpp:344-347; here each GPU reads its own copy), built side by side by the device threads.
+extern "C" int rt_create(const rt_scene_desc* desc, const int* devices, int ndev, rt_ctx** out) {
+    if (!desc || !out || !devices || ndev <= 0) {
+        set_error("rt_create: null argument or empty device list");
+        return RT_ERR_INVALID;
+    }
+    *out = nullptr;
+    int nvis = 0;
+    const hipError_t de = hipGetDeviceCount(&nvis);
+    if (de != hipSuccess || nvis == 0) {
+        set_error(std::string("rt_create: no HIP device available (the MI355X path has no CPU fallback): ") +
+                  (de != hipSuccess ? hipGetErrorString(de) : "0 devices"));
+        return RT_ERR_NO_DEVICE;
+    }
+    for (int i = 0; i < ndev; ++i)
+        if (devices[i] < 0 || devices[i] >= nvis) {
+            set_error("rt_create: device index out of range");
+            return RT_ERR_INVALID;
+        }
+    std::vector<rt_ctx*> reps(ndev, nullptr);
+    std::vector<int> rcs(ndev, RT_OK);
+    std::vector<std::string> errs(ndev);
+    std::vector<std::unique_ptr<DeviceWorker>> workers(ndev);
+    for (int i = 1; i < ndev; ++i) {
+        workers[i].reset(new DeviceWorker());
+        workers[i]->post([&, i] {
+            rcs[i] = create_one(desc, devices[i], &reps[i]);
+            if (rcs[i] != RT_OK) errs[i] = last_error_text();
+        });
+    }
+    rcs[0] = create_one(desc, devices[0], &reps[0]);
+    if (rcs[0] != RT_OK) errs[0] = last_error_text();
+    for (int i = 1; i < ndev; ++i) workers[i]->wait();
+    int rc = RT_OK;
+    std::string err;
+    for (int i = 0; i < ndev && rc == RT_OK; ++i)
+        if (rcs[i] != RT_OK) {
+            rc = rcs[i];
+            err = errs[i];
+        }
+    // the other devices write their pixels straight into devices[0]'s images: peer access to it
+    for (int i = 1; i < ndev && rc == RT_OK; ++i) {
+        if (devices[i] == devices[0]) continue;
+        int can = 0;
+        hipSetDevice(devices[i]);
+        if (hipDeviceCanAccessPeer(&can, devices[i], devices[0]) != hipSuccess || !can) {
+            rc = RT_ERR_HIP;
+            err = "rt_create: device " + std::to_string(devices[i]) + " has no peer access to device " +
+                  std::to_string(devices[0]);
+            break;
+        }
+        const hipError_t e = hipDeviceEnablePeerAccess(devices[0], 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
+            rc = RT_ERR_HIP;
+            err = std::string("rt_create: hipDeviceEnablePeerAccess: ") + hipGetErrorString(e);
+        }
+        (void)hipGetLastError();  // (an already-enabled peer leaves a sticky status)
+    }
+    for (int i = 0; i < ndev && rc == RT_OK; ++i) {
+        hipSetDevice(devices[i]);
+        if (hipEventCreateWithFlags(&reps[i]->ev_done, hipEventDisableTiming) != hipSuccess ||
+            (i == 0 && hipEventCreateWithFlags(&reps[0]->ev_ready, hipEventDisableTiming) != hipSuccess)) {
+            rc = RT_ERR_HIP;
+            err = "rt_create: hipEventCreate failed";
+        }
+    }
+    if (rc != RT_OK) {
+        workers.clear();
+        for (rt_ctx* r : reps) rt_destroy(r);
+        set_error(err);
+        return rc;
+    }
+    rt_ctx* c = reps[0];
+    c->devices.assign(devices, devices + ndev);
+    c->replicas = reps;
+    c->workers = std::move(workers);
+    hipSetDevice(devices[0]);
+    *out = c;
+    return RT_OK;
+}
+
+extern "C" int rt_ctx_devices(rt_ctx* c, int* out, int n) {
+    if (!c) {
+        set_error("rt_ctx_devices: null ctx");
+        return RT_ERR_INVALID;
+    }
+    const int nd = (int)c->devices.size();
+    for (int i = 0; i < n && i < nd && out; ++i) out[i] = c->devices[i];
+    return nd;
+}
+
 // developer / test hooks of the scene build (include/rt_amd.h)
 extern "C" int rt_set_build_mode(int mode) {
     if (mode < 0 || mode > 2) {
@@ -561,22 +722,29 @@ extern "C" int rt_update_lights(rt_ctx* c, const rt_scene_desc* desc) {
         set_error("rt_update_lights: invalid argument");
         return RT_ERR_INVALID;
     }
+    for (rt_ctx* r : c->replicas) {
+        // renders run on the caller's streams: wait for every one in flight on the device, so none reads
+        // a half-replaced array (the ordering contract in rt_amd.h)
+        HIP_TRY(hipSetDevice(r->device));
+        HIP_TRY(hipDeviceSynchronize());
+        const int rc = upload_lights(r, desc);
+        if (rc != RT_OK) return rc;
+    }
     HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    return upload_lights(c, desc);
+    return RT_OK;
 }
 
 // Material edits (kd, ks, shininess, transparency of a mesh or a sphere) after the BVH exists: the
 // reference's BVH and shadow culling do not depend on materials, so nothing is rebuilt.
-extern "C" int rt_update_materials(rt_ctx* c, int num_meshes, const rt_material* materials, int num_spheres,
-                                   const rt_material* sphere_materials) {
+static int update_materials_one(rt_ctx* c, int num_meshes, const rt_material* materials, int num_spheres,
+                                const rt_material* sphere_materials) {
     if (!c || num_meshes != c->nmesh || num_spheres != c->S.nsph || (num_meshes > 0 && !materials) ||
         (num_spheres > 0 && !sphere_materials)) {
         set_error("rt_update_materials: counts must match the context's meshes and spheres");
         return RT_ERR_INVALID;
     }
     HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipDeviceSynchronize());  // every render in flight on the device (caller streams), see rt_amd.h
     bool all_opaque = true, glossy = false;
     std::vector<DMat> mats;
     device_materials(materials, num_meshes, mats, all_opaque, glossy);
@@ -589,17 +757,25 @@ extern "C" int rt_update_materials(rt_ctx* c, int num_meshes, const rt_material*
     if (!sph.empty())
         HIP_TRY(hipMemcpy(const_cast<DSph*>(c->S.sph), sph.data(), sph.size() * sizeof(DSph), hipMemcpyHostToDevice));
     c->S.all_opaque = all_opaque ? 1 : 0;
-    c->glossy_material = glossy;
-    for (int m = 0; m < num_meshes; ++m)  // a texture binding cannot change here (textures are uploaded once)
-        (void)m;
+    c->glossy_material = glossy;  // (texture bindings cannot change here: textures are uploaded once)
     return RT_OK;
 }
 
-extern "C" int rt_ctx_set_option(rt_ctx* c, int option, int value) {
+extern "C" int rt_update_materials(rt_ctx* c, int num_meshes, const rt_material* materials, int num_spheres,
+                                   const rt_material* sphere_materials) {
     if (!c) {
-        set_error("rt_ctx_set_option: null ctx");
+        set_error("rt_update_materials: null ctx");
         return RT_ERR_INVALID;
     }
+    for (rt_ctx* r : c->replicas) {
+        const int rc = update_materials_one(r, num_meshes, materials, num_spheres, sphere_materials);
+        if (rc != RT_OK) return rc;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    return RT_OK;
+}
+
+static int set_option_one(rt_ctx* c, int option, int value) {
     switch (option) {
         case RT_OPT_KERNEL:
             if (value < RT_KERNEL_AUTO || value > RT_KERNEL_DYNAMIC_FETCH) break;
@@ -650,6 +826,18 @@ extern "C" int rt_ctx_set_option(rt_ctx* c, int option, int value) {
     }
     set_error("rt_ctx_set_option: value out of range");
     return RT_ERR_INVALID;
+}
+
+extern "C" int rt_ctx_set_option(rt_ctx* c, int option, int value) {
+    if (!c) {
+        set_error("rt_ctx_set_option: null ctx");
+        return RT_ERR_INVALID;
+    }
+    for (rt_ctx* r : c->replicas) {
+        const int rc = set_option_one(r, option, value);
+        if (rc != RT_OK) return rc;
+    }
+    return RT_OK;
 }
 
 
@@ -974,6 +1162,36 @@ extern "C" int rt_set_counting(int on) {
     return RT_OK;
 }
 
+// A view batch's camera table (12 floats per view: position, quat, hh, hw) into the context's device
+// array, copied on the render's stream from pinned staging that outlives the call (the staging is
+// refilled only after the previous batch's copy has read it).
+static int upload_views(rt_ctx* c, const rt_camera* cams, int n_views, hipStream_t st, KParams& K) {
+    const size_t bytes = (size_t)n_views * 12 * sizeof(float);
+    int rc = ensure(c, &c->d_views, &c->views_bytes, bytes);
+    if (rc != RT_OK) return rc;
+    if (c->ev_views) HIP_TRY(hipEventSynchronize(c->ev_views));
+    else HIP_TRY(hipEventCreateWithFlags(&c->ev_views, hipEventDisableTiming));
+    if (c->h_views_bytes < bytes) {
+        if (c->h_views) HIP_TRY(hipHostFree(c->h_views));
+        c->h_views = nullptr;
+        c->h_views_bytes = 0;
+        HIP_TRY(hipHostMalloc((void**)&c->h_views, bytes, hipHostMallocDefault));
+        c->h_views_bytes = bytes;
+    }
+    for (int i = 0; i < n_views; ++i) {
+        float* o = c->h_views + 12 * i;
+        for (int k = 0; k < 3; ++k) o[k] = cams[i].position[k];
+        for (int k = 0; k < 4; ++k) o[3 + k] = cams[i].quat[k];
+        o[7] = cams[i].half_height;
+        o[8] = cams[i].half_width;
+        o[9] = o[10] = o[11] = 0.0f;
+    }
+    HIP_TRY(hipMemcpyAsync(c->d_views, c->h_views, bytes, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipEventRecord(c->ev_views, st));
+    K.views = reinterpret_cast<const float*>(c->d_views);
+    return RT_OK;
+}
+
 extern "C" int rt_render_device(rt_ctx* c, const rt_camera* cam, const rt_params* p, int W, int H, int band_rows,
                                 int band_rank, int band_count, float* d_out, void* stream, rt_stats* stats) {
     if (!c || !cam || !p || !d_out || W <= 0 || H <= 0 || band_rows <= 0 || band_count <= 0 || band_rank < 0 ||
@@ -1026,20 +1244,107 @@ extern "C" int rt_render_views_device(rt_ctx* c, const rt_camera* cams, int n_vi
     // band_count ranks' buffers gather into one [rank][view][band][row] array whatever rank renders
     // fewer bands (rt_unpermute_views_device)
     K.view_rows = ((nbands + band_count - 1) / band_count) * band_rows;
-    std::vector<float> v((size_t)n_views * 12, 0.0f);
-    for (int i = 0; i < n_views; ++i) {
-        float* o = v.data() + 12 * i;
-        for (int k = 0; k < 3; ++k) o[k] = cams[i].position[k];
-        for (int k = 0; k < 4; ++k) o[3 + k] = cams[i].quat[k];
-        o[7] = cams[i].half_height;
-        o[8] = cams[i].half_width;
-    }
-    rc = ensure(c, &c->d_views, &c->views_bytes, v.size() * sizeof(float));
-    if (rc != RT_OK) return rc;
     hipStream_t st = (hipStream_t)stream;  // NULL: the null stream, ordered with the caller's default-stream work
-    HIP_TRY(hipMemcpyAsync(c->d_views, v.data(), v.size() * sizeof(float), hipMemcpyHostToDevice, st));
-    K.views = reinterpret_cast<const float*>(c->d_views);
+    rc = upload_views(c, cams, n_views, st, K);
+    if (rc != RT_OK) return rc;
     return launch_render(c, K, st, g_count_mode, stats);
+}
+
+// One replica's part of an image-layout render: the bands b with b % band_count == band_rank of every
+// view, each pixel written to its setPixel place in d_images (on this device or a peer's).
+static int launch_image(rt_ctx* c, const rt_camera* cams, int n_views, const rt_params* p, int W, int H,
+                        int band_rows, int band_rank, int band_count, float* d_images, hipStream_t st, rt_stats* stats) {
+    HIP_TRY(hipSetDevice(c->device));
+    KParams K;
+    int rc = fill_params(c, cams, p, W, H, K);
+    if (rc != RT_OK) return rc;
+    const int nbands = (H + band_rows - 1) / band_rows;
+    K.band_rows = band_rows;
+    K.band_rank = band_rank;
+    K.band_count = band_count;
+    K.n_local_bands = nbands > band_rank ? (nbands - band_rank + band_count - 1) / band_count : 0;
+    const long long view_jobs = (long long)((W + 7) / 8) * ((band_rows + 7) / 8) * K.n_local_bands * 64;
+    if (view_jobs * n_views > 0x7FFFFFFFll || (long long)W * H * n_views * 3 >= (1ll << 40)) {
+        set_error("image-layout render: batch too large (job index overflows int)");
+        return RT_ERR_INVALID;
+    }
+    K.out = d_images;
+    K.out_image = 1;
+    K.view_rows = H;
+    K.n_views = n_views;
+    if (n_views > 1) {
+        rc = upload_views(c, cams, n_views, st, K);
+        if (rc != RT_OK) return rc;
+    }
+    return launch_render(c, K, st, g_count_mode, stats);
+}
+
+static void add_stats(rt_stats& a, const rt_stats& b) {
+    a.rays += b.rays;
+    a.node_visits += b.node_visits;
+    a.tri_tests += b.tri_tests;
+    a.hits += b.hits;
+    a.ub_hits += b.ub_hits;
+    a.kernel_ms = std::max(a.kernel_ms, b.kernel_ms);
+}
+
+// renderRayTracing's pixel loop split over the context's devices (the OpenMP row split of
+// src/main.cpp:344-347, here interleaved 8-row bands): replica i renders the caller's bands
+// b % band_count == band_rank that also have (b / band_count) % n == i, on its own stream, ordered
+// after the caller stream's earlier work (ev_ready) and before its later work (ev_done), every pixel
+// stored straight into d_images on devices[0].  No gather and no un-permute: the pixels land where
+// setPixel puts them while the frame renders.
+static int render_split(rt_ctx* c, const rt_camera* cams, int n_views, const rt_params* p, int W, int H,
+                        int band_rows, int band_rank, int band_count, float* d_images, hipStream_t st,
+                        rt_stats* stats) {
+    const int n = std::max<int>(1, (int)c->replicas.size());
+    if (n == 1) return launch_image(c, cams, n_views, p, W, H, band_rows, band_rank, band_count, d_images, st, stats);
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipEventRecord(c->ev_ready, st));
+    std::vector<rt_stats> rs(n);
+    std::vector<int> rcs(n, RT_OK);
+    std::vector<std::string> errs(n);
+    const int count = band_count * n;
+    for (int i = 1; i < n; ++i) {
+        c->workers[i]->post([&, i] {
+            rt_ctx* r = c->replicas[i];
+            rcs[i] = hipSetDevice(r->device) == hipSuccess && hipStreamWaitEvent(r->stream, c->ev_ready, 0) == hipSuccess
+                         ? RT_OK : RT_ERR_HIP;
+            if (rcs[i] == RT_OK)
+                rcs[i] = launch_image(r, cams, n_views, p, W, H, band_rows, band_rank + band_count * i, count, d_images,
+                                      r->stream, stats ? &rs[i] : nullptr);
+            if (rcs[i] == RT_OK && hipEventRecord(r->ev_done, r->stream) != hipSuccess) rcs[i] = RT_ERR_HIP;
+            if (rcs[i] != RT_OK) errs[i] = last_error_text();
+        });
+    }
+    rcs[0] = launch_image(c, cams, n_views, p, W, H, band_rows, band_rank, count, d_images, st, stats ? &rs[0] : nullptr);
+    if (rcs[0] != RT_OK) errs[0] = last_error_text();
+    for (int i = 1; i < n; ++i) c->workers[i]->wait();
+    HIP_TRY(hipSetDevice(c->device));
+    for (int i = 1; i < n; ++i)
+        if (rcs[i] == RT_OK) HIP_TRY(hipStreamWaitEvent(st, c->replicas[i]->ev_done, 0));
+    for (int i = 0; i < n; ++i)
+        if (rcs[i] != RT_OK) {
+            set_error(errs[i].empty() ? "split render failed on device " + std::to_string(c->devices[i]) : errs[i]);
+            return rcs[i];
+        }
+    if (stats) {
+        *stats = rs[0];
+        for (int i = 1; i < n; ++i) add_stats(*stats, rs[i]);
+    }
+    return RT_OK;
+}
+
+extern "C" int rt_render_views_image_device(rt_ctx* c, const rt_camera* cams, int n_views, const rt_params* p, int W,
+                                            int H, int band_rows, int band_rank, int band_count, float* d_images,
+                                            void* stream, rt_stats* stats) {
+    if (!c || !cams || n_views <= 0 || !p || !d_images || W <= 0 || H <= 0 || band_rows <= 0 || band_count <= 0 ||
+        band_rank < 0 || band_rank >= band_count) {
+        set_error("rt_render_views_image_device: invalid argument");
+        return RT_ERR_INVALID;
+    }
+    return render_split(c, cams, n_views, p, W, H, band_rows, band_rank, band_count, d_images, (hipStream_t)stream,
+                        stats);
 }
 
 extern "C" int rt_unpermute_bands_device(int W, int H, int band_rows, int band_count, const float* d_gathered,
@@ -1078,25 +1383,11 @@ extern "C" int rt_render(rt_ctx* c, const rt_camera* cam, const rt_params* p, in
         set_error("rt_render: invalid argument");
         return RT_ERR_INVALID;
     }
-    HIP_TRY(hipSetDevice(c->device));
-    const int band_rows = 8;
-    const int nbands = (H + band_rows - 1) / band_rows;
-    const size_t fb = (size_t)nbands * band_rows * W * 3 * sizeof(float);
-    int rc = ensure(c, &c->d_fb, &c->fb_bytes, fb);
-    if (rc != RT_OK) return rc;
-    rc = ensure(c, &c->d_img, &c->img_bytes, (size_t)W * H * 3 * sizeof(float));
-    if (rc != RT_OK) return rc;
-    rt_stats local{};
-    rc = rt_render_device(c, cam, p, W, H, band_rows, 0, 1, c->d_fb, c->stream, &local);
-    if (rc != RT_OK) return rc;
-    rc = rt_unpermute_bands_device(W, H, band_rows, 1, c->d_fb, c->d_img, c->stream);
-    if (rc != RT_OK) return rc;
-    HIP_TRY(hipMemcpyAsync(rgb_out, c->d_img, (size_t)W * H * 3 * sizeof(float), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    if (stats) *stats = local;
-    return RT_OK;
+    return rt_render_views(c, cam, 1, p, W, H, rgb_out, stats);
 }
 
+// renderRayTracing for a batch of cameras to host memory: every device of the context renders its
+// bands straight into the images on devices[0], which are then copied out.
 extern "C" int rt_render_views(rt_ctx* c, const rt_camera* cams, int n_views, const rt_params* p, int W, int H,
                                float* rgb_out, rt_stats* stats) {
     if (!c || !cams || n_views <= 0 || !p || !rgb_out || W <= 0 || H <= 0) {
@@ -1104,21 +1395,12 @@ extern "C" int rt_render_views(rt_ctx* c, const rt_camera* cams, int n_views, co
         return RT_ERR_INVALID;
     }
     HIP_TRY(hipSetDevice(c->device));
-    const int band_rows = 8;
-    const int nbands = (H + band_rows - 1) / band_rows;
-    const size_t view_fb = (size_t)nbands * band_rows * W * 3;
     const size_t view_img = (size_t)W * H * 3;
-    int rc = ensure(c, &c->d_fb, &c->fb_bytes, view_fb * n_views * sizeof(float));
-    if (rc != RT_OK) return rc;
-    rc = ensure(c, &c->d_img, &c->img_bytes, view_img * n_views * sizeof(float));
+    int rc = ensure(c, &c->d_img, &c->img_bytes, view_img * n_views * sizeof(float));
     if (rc != RT_OK) return rc;
     rt_stats local{};
-    rc = rt_render_views_device(c, cams, n_views, p, W, H, band_rows, 0, 1, c->d_fb, c->stream, &local);
+    rc = render_split(c, cams, n_views, p, W, H, 8, 0, 1, c->d_img, c->stream, &local);
     if (rc != RT_OK) return rc;
-    for (int v = 0; v < n_views; ++v) {
-        rc = rt_unpermute_bands_device(W, H, band_rows, 1, c->d_fb + v * view_fb, c->d_img + v * view_img, c->stream);
-        if (rc != RT_OK) return rc;
-    }
     HIP_TRY(hipMemcpyAsync(rgb_out, c->d_img, view_img * n_views * sizeof(float), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (stats) *stats = local;
@@ -1304,5 +1586,74 @@ extern "C" int rt_selftest_math(rt_ctx* c, const float* x, const float* y, int n
     hipFree(dx);
     hipFree(dy);
     hipFree(dout);
+    return RT_OK;
+}
+
+// ---- device buffers shared across processes (the one-process-per-GPU split, bench.py N > 1) ----
+// Rank 0 allocates the images and exports them; every rank opens them and renders its bands straight
+// into them (rt_render_views_image_device), so the framebuffer exchange is the kernels' own pixel
+// stores over xGMI while they render -- no gather step after the frame.
+extern "C" int rt_ipc_alloc(int device, size_t bytes, void** d_ptr, uint8_t handle[RT_IPC_HANDLE_BYTES]) {
+    if (!d_ptr || !handle || bytes == 0) {
+        set_error("rt_ipc_alloc: invalid argument");
+        return RT_ERR_INVALID;
+    }
+    *d_ptr = nullptr;
+    HIP_TRY(hipSetDevice(device));
+    void* p = nullptr;
+    HIP_TRY(hipMalloc(&p, bytes));
+    hipIpcMemHandle_t h;
+    const hipError_t e = hipIpcGetMemHandle(&h, p);
+    if (e != hipSuccess) {
+        hipFree(p);
+        set_error(std::string("rt_ipc_alloc: hipIpcGetMemHandle: ") + hipGetErrorString(e));
+        return RT_ERR_HIP;
+    }
+    static_assert(sizeof(h) == RT_IPC_HANDLE_BYTES, "IPC handle size");
+    std::memcpy(handle, &h, RT_IPC_HANDLE_BYTES);
+    *d_ptr = p;
+    return RT_OK;
+}
+
+extern "C" int rt_ipc_open(int device, const uint8_t handle[RT_IPC_HANDLE_BYTES], void** d_ptr) {
+    if (!d_ptr || !handle) {
+        set_error("rt_ipc_open: invalid argument");
+        return RT_ERR_INVALID;
+    }
+    *d_ptr = nullptr;
+    HIP_TRY(hipSetDevice(device));
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, handle, RT_IPC_HANDLE_BYTES);
+    HIP_TRY(hipIpcOpenMemHandle(d_ptr, h, hipIpcMemLazyEnablePeerAccess));
+    return RT_OK;
+}
+
+extern "C" int rt_ipc_close(void* d_ptr) {
+    if (!d_ptr) return RT_OK;
+    HIP_TRY(hipIpcCloseMemHandle(d_ptr));
+    return RT_OK;
+}
+
+extern "C" int rt_device_free(int device, void* d_ptr) {
+    if (!d_ptr) return RT_OK;
+    HIP_TRY(hipSetDevice(device));
+    HIP_TRY(hipFree(d_ptr));
+    return RT_OK;
+}
+
+// Wait for every stream of the device (the split render's device threads enqueue on their own streams).
+extern "C" int rt_device_synchronize(int device) {
+    HIP_TRY(hipSetDevice(device));
+    HIP_TRY(hipDeviceSynchronize());
+    return RT_OK;
+}
+
+// Synchronous device-to-host copy (a buffer this library allocated or opened, e.g. rt_ipc_alloc's).
+extern "C" int rt_memcpy_dtoh(void* host, const void* d_ptr, size_t bytes) {
+    if ((!host || !d_ptr) && bytes) {
+        set_error("rt_memcpy_dtoh: null pointer");
+        return RT_ERR_INVALID;
+    }
+    HIP_TRY(hipMemcpy(host, d_ptr, bytes, hipMemcpyDeviceToHost));
     return RT_OK;
 }

@@ -16,6 +16,10 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 LIB_PATH = os.path.join(HERE, "librt_amd.so")
+# tools/sanitize/run.sh only: the CPU-only ASan/UBSan build of the host sources (its GPU entries are stubs
+# that fail with RT_ERR_NO_DEVICE, so nothing can pass on it that needs the GPU path)
+if os.environ.get("RT_AMD_SANITIZER_LIB"):
+    LIB_PATH = os.environ["RT_AMD_SANITIZER_LIB"]
 SCENE_DIR = os.path.join(REPO, "tests", "golden", "scenes")
 
 FLT_MAX = float(np.finfo(np.float32).max)
@@ -130,7 +134,10 @@ EXPORTS = [
     "rt_postprocess_device", "rt_bitmap_device", "rt_postprocess", "rt_bitmap", "rt_encode_bmp", "rt_write_bmp",
     "rt_philox4x32_10", "rt_debug_wave_trace", "rt_debug_job_trace", "rt_debug_create_ms", "rt_set_build_mode", "rt_debug_build_info", "rt_debug_records", "rt_decode_png", "rt_ctx_set_option", "rt_texture_sample",
     "rt_update_lights", "rt_update_materials", "rt_unpermute_views_device", "rt_scene_mesh_count", "rt_scene_mesh_get",
+    "rt_ctx_devices", "rt_render_views_image_device", "rt_ipc_alloc", "rt_ipc_open", "rt_ipc_close", "rt_device_free",
+    "rt_device_synchronize", "rt_memcpy_dtoh",
 ]
+IPC_HANDLE_BYTES = 64
 
 BUILD_AUTO, BUILD_HOST, BUILD_GPU = 0, 1, 2
 
@@ -242,7 +249,16 @@ def lib():
             "rt_write_dragon_proxy": ([C.c_char_p, C.c_int, C.c_int], C.c_int),
             "rt_camera_from_trackball": ([P(C.c_float), P(C.c_float), C.c_float, C.c_float, C.c_float,
                                          P(rt_camera)], C.c_int),
-            "rt_create": ([P(rt_scene_desc), C.c_int, P(vp)], C.c_int),
+            "rt_create": ([P(rt_scene_desc), P(C.c_int), C.c_int, P(vp)], C.c_int),
+            "rt_ctx_devices": ([vp, P(C.c_int), C.c_int], C.c_int),
+            "rt_render_views_image_device": ([vp, P(rt_camera), C.c_int, P(rt_params), C.c_int, C.c_int, C.c_int,
+                                              C.c_int, C.c_int, vp, vp, P(rt_stats)], C.c_int),
+            "rt_ipc_alloc": ([C.c_int, C.c_size_t, P(vp), P(C.c_uint8)], C.c_int),
+            "rt_ipc_open": ([C.c_int, P(C.c_uint8), P(vp)], C.c_int),
+            "rt_ipc_close": ([vp], C.c_int),
+            "rt_device_free": ([C.c_int, vp], C.c_int),
+            "rt_device_synchronize": ([C.c_int], C.c_int),
+            "rt_memcpy_dtoh": ([vp, vp, C.c_size_t], C.c_int),
             "rt_destroy": ([vp], C.c_int),
             "rt_render": ([vp, P(rt_camera), P(rt_params), C.c_int, C.c_int, P(C.c_float), P(rt_stats)], C.c_int),
             "rt_render_device": ([vp, P(rt_camera), P(rt_params), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
@@ -460,13 +476,17 @@ def decode_png(data):
 
 
 class Context:
-    """Device context = BoundingVolumeHierarchy(Scene*) + uploaded scene (one GPU)."""
+    """Device context = BoundingVolumeHierarchy(Scene*) + uploaded scene: one GPU (`device`), or one scene
+    replica per entry of `devices` (renders split their bands over them)."""
 
-    def __init__(self, scene, device=0):
+    def __init__(self, scene, device=0, devices=None):
         self.scene = scene  # keep the host scene alive (desc points into it)
         self.h = C.c_void_p()
         d = scene.desc()
-        check(lib().rt_create(C.byref(d), int(device), C.byref(self.h)), "rt_create")
+        devs = [int(device)] if devices is None else [int(x) for x in devices]
+        arr = (C.c_int * len(devs))(*devs)
+        check(lib().rt_create(C.byref(d), arr, len(devs), C.byref(self.h)), "rt_create")
+        self.devices = devs
 
     def close(self):
         if getattr(self, "h", None) and self.h.value:
@@ -534,6 +554,18 @@ class Context:
                                            C.byref(st)), "rt_render_views_device")
         return st
 
+    def render_views_image_device(self, cams, prm, W, H, d_images_ptr, stream_ptr=None, band_rows=8, band_rank=0,
+                                  band_count=1, stats=True):
+        """rt_render_views_image_device: the views' pixels straight into d_images (setPixel layout, view v at
+        v*W*H*3), split over the context's devices; this call renders bands b % band_count == band_rank.
+        stats=False keeps the call asynchronous on the stream (returns None)."""
+        arr = (rt_camera * len(cams))(*cams)
+        st = rt_stats() if stats else None
+        check(lib().rt_render_views_image_device(self.h, arr, len(cams), C.byref(prm), W, H, band_rows, band_rank,
+                                                 band_count, C.c_void_p(d_images_ptr), C.c_void_p(stream_ptr or 0),
+                                                 C.byref(st) if stats else None), "rt_render_views_image_device")
+        return st
+
     def intersect(self, rays, use_bvh):
         rays = np.ascontiguousarray(rays, dtype=RAY_DTYPE)
         hits = np.zeros(len(rays), HIT_DTYPE)
@@ -590,6 +622,45 @@ class Context:
 
 def set_counting(on):
     check(lib().rt_set_counting(int(on)))
+
+
+class IpcBuffer:
+    """Device memory shared across processes (rt_ipc_alloc / rt_ipc_open): the owner allocates and exports
+    a handle (bytes), other processes open it; .ptr is the device address in this process."""
+
+    def __init__(self, device, nbytes=None, handle=None):
+        self.device = int(device)
+        self.ptr = None
+        self.owner = handle is None
+        p = C.c_void_p()
+        if self.owner:
+            h = (C.c_uint8 * IPC_HANDLE_BYTES)()
+            check(lib().rt_ipc_alloc(self.device, int(nbytes), C.byref(p), h), "rt_ipc_alloc")
+            self.handle = bytes(h)
+        else:
+            h = (C.c_uint8 * IPC_HANDLE_BYTES).from_buffer_copy(bytes(handle))
+            check(lib().rt_ipc_open(self.device, h, C.byref(p)), "rt_ipc_open")
+            self.handle = bytes(handle)
+        self.ptr = p.value
+
+    def close(self):
+        if self.ptr:
+            if self.owner:
+                lib().rt_device_free(self.device, C.c_void_p(self.ptr))
+            else:
+                lib().rt_ipc_close(C.c_void_p(self.ptr))
+            self.ptr = None
+
+
+def device_to_host(d_ptr, n):
+    """n float32 from device memory (e.g. an IpcBuffer) to a new host array (synchronous)."""
+    out = np.empty(int(n), np.float32)
+    check(lib().rt_memcpy_dtoh(out.ctypes.data, C.c_void_p(d_ptr), out.nbytes), "rt_memcpy_dtoh")
+    return out
+
+
+def device_synchronize(device):
+    check(lib().rt_device_synchronize(int(device)), "rt_device_synchronize")
 
 
 # --------------------------------------------------------------------------------------------

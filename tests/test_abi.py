@@ -31,7 +31,7 @@ def test_library_exports_every_symbol(R):
 
 
 def test_abi_version_and_struct_sizes(R):
-    assert R.lib().rt_abi_version() == 4
+    assert R.lib().rt_abi_version() == 5
     assert ctypes.sizeof(R.rt_stats) == 112
     assert ctypes.sizeof(R.rt_material) == 40
     assert ctypes.sizeof(R.rt_ray) == 28

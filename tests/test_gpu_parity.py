@@ -160,7 +160,7 @@ def test_ub_regime_count_matches_oracle(R, O, ctxs, cfg, uv, W, H):
     assert st.ub_hits <= st.hits
 
 
-@pytest.mark.parametrize("cfg,uv", [("C3", (200, 80)), ("C5", None)])
+@pytest.mark.parametrize("cfg,uv", [("C3", (200, 80)), ("C4", (200, 80)), ("C5", None)])
 def test_band_split_bit_identical(R, ctxs, cfg, uv):
     """The multi-GPU layout (interleaved 8-row bands per rank + un-permute) reproduces the
     single-GPU frame bit for bit, and a re-render is deterministic."""
@@ -193,7 +193,7 @@ def test_band_split_bit_identical(R, ctxs, cfg, uv):
         assert rays == st.rays
 
 
-@pytest.mark.parametrize("cfg,uv", [("C3", (200, 80)), ("C2", None)])
+@pytest.mark.parametrize("cfg,uv", [("C3", (200, 80)), ("C4", (200, 80)), ("C2", None)])
 def test_band_split_view_batch_bit_identical(R, ctxs, cfg, uv):
     """bench.py's N>1 step on one GPU: each rank's bands of every view in one launch, the buffers
     back to back as all_gather_into_tensor leaves them, one rt_unpermute_views_device launch --
