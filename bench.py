@@ -37,6 +37,9 @@ METRIC = "Mrays/s (primary+shadow+secondary) at 1920×1080; fraction of HBM roof
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 BAND_ROWS = 8
 DEFAULT_VIEWS = 64  # frames per step: a 64-view turntable (5.625 deg apart) of the C3 scene in one launch
+# frames per step of the other configs (a step of a few hundred ms at most): C4's 64-sample soft shadows
+# take ~10 ms per frame, C5's 4K frames with 3 x 64 plane-light samples ~0.2 s
+CONFIG_VIEWS = {"C1": 64, "C2": 64, "C3": DEFAULT_VIEWS, "C4": 16, "C5": 2}
 
 
 def algorithmic_bytes(st, pixels):
@@ -120,6 +123,43 @@ def pmc_key(config, views):
     return f"{config}v{views}"
 
 
+def measure_pmc(config, views, kernel, timeout_s=150):
+    """HBM bytes per render launch measured now: two rocprofv3 --pmc passes (FETCH_SIZE, then WRITE_SIZE:
+    together they exceed the 4 TCC counters one pass can hold) over tools/prof_target.py, which makes the
+    same launches this bench times (config, views, library); per MI355X_MICROARCH.md's HBM section
+    FETCH_SIZE and WRITE_SIZE are KB and gfx950's FETCH_SIZE tallies 128-B requests at 64 B, so
+    bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.  Returns (bytes or None, provenance)."""
+    import shutil
+    import subprocess
+    import tempfile
+
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import pmc_summary
+
+    exe = shutil.which("rocprofv3")
+    if not exe:
+        return None, "rocprofv3 not found"
+    med = {}
+    with tempfile.TemporaryDirectory(prefix="bench_pmc_") as tmp:
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            out = os.path.join(tmp, ctr)
+            cmd = ["timeout", "-s", "KILL", str(timeout_s), exe, "--pmc", ctr, "--kernel-trace", "--output-format", "csv",
+                   "-d", out, "-o", "run", "--", sys.executable, os.path.join(REPO, "tools", "prof_target.py"),
+                   config, "2", str(views)]
+            r = subprocess.run(cmd, capture_output=True, text=True, cwd=REPO)
+            if r.returncode != 0:
+                return None, f"rocprofv3 --pmc {ctr} failed (rc {r.returncode}): {(r.stderr or r.stdout)[-300:]}"
+            kname, m = pmc_summary.collect(out)
+            if ctr not in m or not kname or kernel not in kname:
+                return None, f"rocprofv3 --pmc {ctr}: no counter rows for {kernel}"
+            med[ctr] = m[ctr]
+    hbm = (2.0 * med["FETCH_SIZE"] + med["WRITE_SIZE"]) * 1024.0
+    return hbm, (f"measured in this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over tools/prof_target.py "
+                 f"{config} {views} views (the same kernel and library), median per launch; FETCH_SIZE "
+                 f"{med['FETCH_SIZE']:.0f} KB (x2, gfx950 64-B tally of 128-B requests), WRITE_SIZE "
+                 f"{med['WRITE_SIZE']:.0f} KB")
+
+
 def load_pmc(config, kernel, sha, path=None):
     """HBM bytes per render launch from the committed rocprofv3 --pmc summary
     (profiles/pmc_latest.json, written by tools/pmc_summary.py --latest) -- used only when it was
@@ -152,8 +192,8 @@ def main():
                     help="N>1: bands = every view of the step split into interleaved 8-row bands over the ranks, "
                          "RCCL gather to rank 0, un-permute there (north_star's tile split, strong scaling); frames = "
                          "every rank renders its own turntable views (weak scaling, no collective on the data path)")
-    ap.add_argument("--views", type=int, default=DEFAULT_VIEWS,
-                    help="frames per step, rendered in ONE launch (rt_render_views_device)")
+    ap.add_argument("--views", type=int, default=None,
+                    help="frames per step, rendered in ONE launch (default per config: C3 64, C4 16, C5 2)")
     ap.add_argument("--view-step", type=float, default=None,
                     help="turntable step between views in degrees (default 360 / views)")
     ap.add_argument("--exchange", choices=("ipc", "gather"), default="ipc",
@@ -164,7 +204,11 @@ def main():
     ap.add_argument("--resolution", default=None, help="WxH override (tests; the BENCH line uses the config's)")
     ap.add_argument("--dragon-uv", default=None, help="UxV dragon-proxy tessellation override (tests)")
     ap.add_argument("--dump-images", default=None, help="rank 0 saves the last step's images (.npy; tests)")
+    ap.add_argument("--no-pmc", action="store_true",
+                    help="skip the two rocprofv3 --pmc passes that measure roofline.traffic (N = 1)")
     args = ap.parse_args()
+    if args.views is None:
+        args.views = CONFIG_VIEWS.get(args.config, DEFAULT_VIEWS)
 
     import torch
     import torch.distributed as dist
@@ -344,7 +388,15 @@ def main():
         achieved = bytes0 / (avg_ms * 1e-3) / 1e9
         kname = st.kernel_name
         sha = lib_sha()
-        pmc, pmc_src = load_pmc(pmc_key(args.config, F), kname, sha)
+        pmc, pmc_src = None, "not measured (--no-pmc or N > 1)"
+        if world == 1 and not args.no_pmc and not args.resolution and not args.dragon_uv:
+            pmc, pmc_src = measure_pmc(args.config, F, kname)
+        if pmc is None:  # the committed summary, if it was measured on this exact library build
+            pmc_c, src_c = load_pmc(pmc_key(args.config, F), kname, sha)
+            if pmc_c is not None:
+                pmc, pmc_src = pmc_c, src_c
+            else:
+                pmc_src += f"; {src_c}"
         line = {
             "metric": METRIC,
             "value": total_rays / max_elapsed / 1e6,

@@ -230,11 +230,16 @@ int rt_decode_png(const uint8_t* data, long size, int* width, int* height, int* 
 int rt_last_error(char* buf, size_t len);
 
 /* ---- scene ingest (host) ---- */
-/* loadMesh (src/mesh.cpp:58-188) with Assimp 5.0.1 OBJ semantics; appends the meshes to scene. */
+/* loadMesh (src/mesh.cpp:58-188) with Assimp 5.0.1 OBJ semantics; appends the meshes to scene.
+ * assimp3_compat: 0 for 5.0.1 (the reference's pinned version), or bits of Assimp 3.x behaviour that 5.0.1
+ * is believed to have dropped: shininess = 4 x Ns, and GenNormals face normals
+ * normalised by division (x / |n|) instead of by the reciprocal (x * (1 / |n|)). */
+#define RT_ASSIMP3_SHININESS_X4 1
+#define RT_ASSIMP3_NORMALS_DIV 2
 int rt_scene_new(rt_scene** out);
-int rt_scene_load_obj(rt_scene* scene, const char* path, int normalize, int shininess_x4);
+int rt_scene_load_obj(rt_scene* scene, const char* path, int normalize, int assimp3_compat);
 /* loadScene presets (src/scene.cpp:4-150).  preset: SceneType enum value (src/scene.h:14-34). */
-int rt_scene_preset(rt_scene* scene, int preset, const char* data_dir, int shininess_x4);
+int rt_scene_preset(rt_scene* scene, int preset, const char* data_dir, int assimp3_compat);
 int rt_scene_add_sphere(rt_scene* scene, const rt_sphere* s);
 int rt_scene_add_point_light(rt_scene* scene, const rt_point_light* l);
 int rt_scene_add_spherical_light(rt_scene* scene, const rt_spherical_light* l);

@@ -64,10 +64,11 @@ struct HostScene {
 
 // loadMesh (src/mesh.cpp:58-162) + centerAndScaleToUnitMesh (:164-188) with Assimp 5.0.1
 // OBJ/MTL importer semantics.  Throws std::runtime_error on failure.
-std::vector<Mesh> load_obj(const std::string& path, bool normalize, bool shininess_x4);
+// compat: RT_ASSIMP3_* bits (rt_amd.h)
+std::vector<Mesh> load_obj(const std::string& path, bool normalize, int compat);
 
 // loadScene (src/scene.cpp:4-150)
-void load_preset(HostScene& scene, int preset, const std::string& data_dir, bool shininess_x4);
+void load_preset(HostScene& scene, int preset, const std::string& data_dir, int compat);
 
 // Deterministic torus-knot stand-in for data/dragon.obj (missing, .MISSING_LARGE_BLOBS:1)
 void write_dragon_proxy(const std::string& obj_path, int u_segments, int v_segments);

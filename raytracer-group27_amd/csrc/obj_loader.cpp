@@ -419,9 +419,12 @@ static v3 ai_normalize(v3 v) {
     const float inv = 1.0f / l;
     return v3{v.x * inv, v.y * inv, v.z * inv};
 }
-static v3 ai_normalize_safe(v3 v) {
+// NormalizeSafe(): 5.x's operator/= multiplies by the reciprocal; 3.x divides each component
+// (RT_ASSIMP3_NORMALS_DIV: bit-exact with the Assimp 3.3 build of this image)
+static v3 ai_normalize_safe(v3 v, bool div = false) {
     const float l = ai_len(v);
     if (l > 0.0f) {
+        if (div) return v3{v.x / l, v.y / l, v.z / l};
         const float inv = 1.0f / l;
         return v3{v.x * inv, v.y * inv, v.z * inv};
     }
@@ -539,7 +542,7 @@ static void ear_cut(const std::vector<v3>& verts, const std::vector<uint32_t>& i
 }
 
 // createTopology + createVertexArray + TriangulateProcess + GenFaceNormalsProcess
-static bool build_ai_mesh(const ObjModel& m, const ObjMesh& om, AiMesh& out) {
+static bool build_ai_mesh(const ObjModel& m, const ObjMesh& om, AiMesh& out, bool normals_div) {
     if (om.faces.empty()) return false;
     out.material = (om.material >= 0) ? om.material : 0;
     out.has_normals = om.has_normals;
@@ -594,7 +597,7 @@ static bool build_ai_mesh(const ObjModel& m, const ObjMesh& om, AiMesh& out) {
     if (!out.has_normals) {
         for (const auto& t : out.tris) {
             const v3 p1 = out.verts[t[0]], p2 = out.verts[t[1]], p3 = out.verts[t[2]];
-            const v3 nor = ai_normalize_safe(ai_cross(p2 - p1, p3 - p1));
+            const v3 nor = ai_normalize_safe(ai_cross(p2 - p1, p3 - p1), normals_div);
             for (int c = 0; c < 3; ++c) out.norms[t[c]] = nor;
         }
         out.has_normals = true;
@@ -660,7 +663,8 @@ static m3 inverse_transpose(const M4& a) {
 
 }  // namespace
 
-std::vector<Mesh> load_obj(const std::string& path, bool normalize, bool shininess_x4) {
+std::vector<Mesh> load_obj(const std::string& path, bool normalize, int compat) {
+    const bool shininess_x4 = (compat & RT_ASSIMP3_SHININESS_X4) != 0, normals_div = (compat & RT_ASSIMP3_NORMALS_DIV) != 0;
     ObjModel model;
     parse_obj(model, path);
     const std::string dir = path.substr(0, path.find_last_of("/\\") + 1);
@@ -675,7 +679,7 @@ std::vector<Mesh> load_obj(const std::string& path, bool normalize, bool shinine
         Node nd;
         for (int mi : o.meshes) {
             AiMesh am;
-            if (build_ai_mesh(model, model.meshes[mi], am)) {
+            if (build_ai_mesh(model, model.meshes[mi], am, normals_div)) {
                 ai_meshes.push_back(std::move(am));
                 nd.meshes.push_back((int)ai_meshes.size() - 1);
             }

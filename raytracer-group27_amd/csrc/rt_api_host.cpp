@@ -60,7 +60,7 @@ extern "C" int rt_scene_load_obj(rt_scene* sc, const char* path, int normalize, 
         return RT_ERR_INVALID;
     }
     try {
-        auto meshes = load_obj(path, normalize != 0, x4 != 0);
+        auto meshes = load_obj(path, normalize != 0, x4);
         for (auto& m : meshes) sc->s.meshes.push_back(std::move(m));
         sc->dirty = true;
         sc->s.load_textures();
@@ -75,7 +75,7 @@ extern "C" int rt_scene_preset(rt_scene* sc, int preset, const char* data_dir, i
         return RT_ERR_INVALID;
     }
     try {
-        load_preset(sc->s, preset, data_dir, x4 != 0);
+        load_preset(sc->s, preset, data_dir, x4);
         sc->dirty = true;
         sc->s.load_textures();
         return RT_OK;

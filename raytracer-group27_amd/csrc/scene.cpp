@@ -152,7 +152,7 @@ enum Preset {
     MikeScene2
 };
 
-void load_preset(HostScene& scene, int preset, const std::string& data_dir, bool x4) {
+void load_preset(HostScene& scene, int preset, const std::string& data_dir, int x4) {
     const std::string d = data_dir.empty() || data_dir.back() == '/' ? data_dir : data_dir + "/";
     switch (preset) {
         case SingleTriangle: {  // src/scene.cpp:9-18

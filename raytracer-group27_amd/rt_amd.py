@@ -140,6 +140,7 @@ EXPORTS = [
 IPC_HANDLE_BYTES = 64
 
 BUILD_AUTO, BUILD_HOST, BUILD_GPU = 0, 1, 2
+ASSIMP3_SHININESS_X4, ASSIMP3_NORMALS_DIV = 1, 2  # rt_scene_load_obj / rt_scene_preset compat bits
 
 
 def set_build_mode(mode):
@@ -337,9 +338,10 @@ class Scene:
             lib().rt_scene_free(self.h)
             self.h = C.c_void_p()
 
-    def load_obj(self, path, normalize=False, shininess_x4=False):
-        check(lib().rt_scene_load_obj(self.h, str(path).encode(), int(normalize), int(shininess_x4)),
-              f"loadMesh({path})")
+    def load_obj(self, path, normalize=False, shininess_x4=False, normals_div=False):
+        """loadMesh; shininess_x4 / normals_div select Assimp 3.x behaviour (RT_ASSIMP3_* in rt_amd.h)."""
+        compat = (ASSIMP3_SHININESS_X4 if shininess_x4 else 0) | (ASSIMP3_NORMALS_DIV if normals_div else 0)
+        check(lib().rt_scene_load_obj(self.h, str(path).encode(), int(normalize), compat), f"loadMesh({path})")
         return self
 
     def preset(self, preset, data_dir, shininess_x4=False):

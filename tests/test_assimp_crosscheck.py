@@ -112,8 +112,45 @@ def test_loader_matches_assimp(R, assimp, name):
         assert j == len(tri), (name, k)
         if name != "AndreasScene.obj":
             assert extra == 0, (name, k)
-        # normals: same GenNormals face normals (file normals where the OBJ has 'vn')
+        # normals (file normals where the OBJ has 'vn', else GenNormals face normals): bit for bit in
+        # test_generated_normals_bit_exact_with_division
         assert float(np.max(np.abs(vert[:, 3:6] - nrm))) <= 1e-6, (name, k)
+
+
+def _ulps(a, b):
+    a = np.ascontiguousarray(a, np.float32).view(np.int32).astype(np.int64)
+    b = np.ascontiguousarray(b, np.float32).view(np.int32).astype(np.int64)
+    return np.abs(a - b).ravel()
+
+
+@pytest.mark.parametrize("name", FILES)
+def test_generated_normals_bit_exact_with_division(R, assimp, name):
+    """Assimp 3.3 normalises GenNormals face normals as x / |n|; with that rule
+    (RT_ASSIMP3_NORMALS_DIV) every normal of every file is bit-identical to 3.3's (teapot.obj: 95 280
+    generated components).  The default is 5.0.1's believed reciprocal form x * (1 / |n|), which
+    differs from 3.3's by exactly 1 ulp where the two roundings disagree (teapot.obj: 26 025 of
+    95 280 components; files with 'vn' are unaffected)."""
+    path = os.path.join(R.data_dir(), name)
+    ref = assimp_meshes(assimp, path)
+    div = R.Scene().load_obj(path, normalize=False, normals_div=True).meshes()
+    rcp = R.Scene().load_obj(path, normalize=False).meshes()
+    hist = {}
+    def z(a):  # loadMesh's normalMatrix * n (src/mesh.cpp:85,113) decides the sign of zero components
+        a = np.array(a, np.float32)
+        a[a == 0] = 0.0
+        return a
+
+    for (pos, nrm, tri), (vd, _, _, _), (vr, _, _, _) in zip(ref, div, rcp):
+        want = z(nrm)
+        assert z(vd[:, 3:6]).tobytes() == want.tobytes(), name
+        u, c = np.unique(_ulps(z(vr[:, 3:6]), want), return_counts=True)
+        for a, b in zip(u, c):
+            hist[int(a)] = hist.get(int(a), 0) + int(b)
+    assert max(hist) <= 1, (name, hist)
+    if name == "teapot.obj":
+        assert hist == {0: 69255, 1: 26025}, hist
+    else:
+        assert set(hist) == {0}, (name, hist)  # file normals ('vn'): no normalisation involved
 
 
 def test_andreas_scene_has_large_polygons(R):

@@ -1,5 +1,6 @@
 """rocprofv3 target: build one config's scene, then render it N times -- the same launches bench.py
-times: one frame (views = 1) or a turntable batch of V views in one launch (bench.py --views V).
+times: one frame (views = 1) or a turntable batch of V views in one launch (bench.py --views V), every pixel
+stored in its setPixel place (rt_render_views_image_device).
 
     python tools/prof_target.py CONFIG N [VIEWS]
 """
@@ -19,8 +20,9 @@ if views == 1:
 else:
     import torch
     cams = R.turntable_cameras(views, R.aspect_of(W, H))
-    buf = torch.zeros(views * R.local_band_elems(W, H, 8, 1), dtype=torch.float32, device="cuda")
+    buf = torch.zeros(views * W * H * 3, dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
     for _ in range(n):
-        st = ctx.render_views_device(cams, p, W, H, 8, 0, 1, buf.data_ptr(), None)
+        st = ctx.render_views_image_device(cams, p, W, H, buf.data_ptr(), None)
     torch.cuda.synchronize()
 print(cfg, "views", views, "rays", st.rays, "kernel_ms", st.kernel_ms, flush=True)
