@@ -954,18 +954,16 @@ __device__ __attribute__((noinline)) bool advance_lane_call(const void* ka, Lane
     return advance_lane<COUNT, TEX>(kernel_params(ka), kernel_jobs(ka), ka, L, fr, hit, b, fan, q, cnt, job_rays);
 }
 
-// Kernel variants (compile-time): bit 0 RT_V_CALL = state machine out of line (with RT_V_NOCOOP); bit 1 RT_V_NOPF = no node prefetch in the dynamic-fetch traversal; bit 2 RT_V_NOCOOP = no drain
-// lane groups; bit 3 RT_V_W3 / bit 4 RT_V_W4 = compiled for 3 / 4 waves per SIMD (168 / 128 VGPRs)
-// instead of 2 (256).  Every variant renders the same bits; they differ in registers, spills and
-// occupancy.
+// Kernel variants (compile-time): bit 0 RT_V_CALL = state machine (and drain lane groups) out of line;
+// bit 1 RT_V_NOPF = no node prefetch in the dynamic-fetch traversal; bit 2 RT_V_NOCOOP = no drain lane
+// groups; bit 4 RT_V_W4 = compiled for 4 waves per SIMD (128 VGPRs) instead of 2 (256); bit 8 RT_V_FAN =
+// light-sample fans.  Every variant renders the same bits; they differ in registers, spills and occupancy.
 #define RT_V_CALL 1
 #define RT_V_NOPF 2
 #define RT_V_NOCOOP 4
-#define RT_V_W3 8
 #define RT_V_W4 16  // compiled for 4 waves per SIMD (128 VGPRs)
-#define RT_V_W5 128  // compiled for 5 waves per SIMD (~100 VGPRs)
 #define RT_V_FAN 256  // dynamic fetch: the spherical-light sample fans compiled in (P.fan)
-#define RT_V_WAVES(V) (((V) & RT_V_W5) ? 5 : ((V) & RT_V_W4) ? 4 : (((V) & RT_V_W3) ? 3 : 2))
+#define RT_V_WAVES(V) (((V) & RT_V_W4) ? 4 : 2)
 
 
 template <bool COUNT, bool TEX, int V>
@@ -1521,6 +1519,19 @@ __device__ __forceinline__ uint2 coop_group_trace(const float4* __restrict__ nod
     return n;
 }
 
+// The drain traversal as an out-of-line call, for the variants whose state machine is out of line
+// (RT_V_CALL): the lane groups' registers are the callee's, not added to the traversal loop's.  Every
+// argument is wave-uniform and the call is made with every lane active (the phase-B loop's exits are
+// wave-uniform), which the lane groups' cross-lane steps need.
+template <int NW>
+__device__ __attribute__((noinline)) uint2 coop_group_trace_call(const float4* __restrict__ nodes,
+                                                                 const float4* __restrict__ tri,
+                                                                 const DRefNode* __restrict__ refn,
+                                                                 const int* __restrict__ leaf_path, int* pool, int* q,
+                                                                 unsigned long long om, int reserve) {
+    return coop_group_trace<NW>(nodes, tri, refn, leaf_path, pool, q, om, reserve);
+}
+
 // Epilogue of trace_query8: the spheres, after every triangle (same order and keys).
 __device__ __forceinline__ void trav_finish(const DevScene& S, Trav& T) {
     if (T.any && T.found) return;
@@ -1614,9 +1625,8 @@ __device__ __forceinline__ void fan_record(FanTable& ft, int f, int s, bool vis,
 
 template <bool COUNT, bool TEX, int V>
 __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParams P, JobSrc J) {
-    // the drain lane groups run inline only: with the out-of-line state machine (RT_V_CALL) the variant
-    // is compiled without them (an out-of-line drain call there lost values the kernel held across it)
-    constexpr bool PF = !(V & RT_V_NOPF), COOP = !(V & (RT_V_NOCOOP | RT_V_CALL)), FANS = (V & RT_V_FAN) != 0;
+    // drain lane groups: inline, or out of line with the out-of-line state machine (RT_V_CALL)
+    constexpr bool PF = !(V & RT_V_NOPF), COOP = !(V & RT_V_NOCOOP), FANS = (V & RT_V_FAN) != 0;
     const bool fan_on = FANS && P.fan;  // (the host sets P.fan only for FANS variants)
     __shared__ int stack_lds[RT_STACK8 * RT_WAVE];
     __shared__ int coop_pool[COOP_POOL];   // drain: node groups of the wave's last queries
@@ -1898,8 +1908,11 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
                         if (T.cur != RT_TRAV_NONE) gp[T.sp] = (int)T.cur;
                     }
                     __syncthreads();
-                    const uint2 nv = coop_group_trace<8>(S.nodes, S.tri, S.refn, S.leaf_path, coop_pool, coop_q, om,
-                                                         P.coop_reserve);
+                    const uint2 nv =
+                        (V & RT_V_CALL) ? coop_group_trace_call<8>(S.nodes, S.tri, S.refn, S.leaf_path, coop_pool,
+                                                                   coop_q, om, P.coop_reserve)
+                                        : coop_group_trace<8>(S.nodes, S.tri, S.refn, S.leaf_path, coop_pool, coop_q,
+                                                              om, P.coop_reserve);
                     __syncthreads();
                     if (COUNT) {
                         cnt.nodes += nv.x;

@@ -869,9 +869,8 @@ static bool use_df(const rt_ctx* c, const KParams& K) {
 #define RT_DF_BATCH (RT_V_CALL | RT_V_NOPF | RT_V_NOCOOP | RT_V_W4)
 #define RT_DF_FRAME 0
 #define RT_WT_DEFAULT 0
-#define RT_DF_ALT1 (RT_V_CALL | RT_V_NOPF | RT_V_NOCOOP | RT_V_W3)
-#define RT_DF_ALT2 (RT_V_CALL | RT_V_NOPF | RT_V_NOCOOP | RT_V_W5)
-#define RT_WT_ALT1 (RT_V_CALL | RT_V_W3)
+// the one A/B alternate: the batch variant with the drain lane groups, called out of line
+#define RT_DF_ALT (RT_V_CALL | RT_V_NOPF | RT_V_W4)
 
 // by render shape: view batches and sample-fan renders run the lean 4-wave variant (C4 single frame
 // with fans: 27.1 vs 30.3 ms), other single frames the 2-wave variant with the drain lane groups
@@ -908,9 +907,7 @@ static int launch_persistent(int grid, hipStream_t st, const KParams& K, const J
     bool ok = tex ? launch_shipped<COUNT, true>(df, v, grid, st, K, J) : launch_shipped<COUNT, false>(df, v, grid, st, K, J);
     if (!ok && !COUNT && !tex) {
         ok = true;
-        if (df && v == RT_DF_ALT1) launch_v<true, false, false, RT_DF_ALT1>(grid, st, K, J);
-        else if (df && v == RT_DF_ALT2) launch_v<true, false, false, RT_DF_ALT2>(grid, st, K, J);
-        else if (!df && v == RT_WT_ALT1) launch_v<false, false, false, RT_WT_ALT1>(grid, st, K, J);
+        if (df && v == RT_DF_ALT) launch_v<true, false, false, RT_DF_ALT>(grid, st, K, J);
         else ok = false;
     }
     if (!ok) {
@@ -945,11 +942,9 @@ static int persistent_grid(rt_ctx* c, const KParams& K) {
         if (v == RT_DF_BATCH) e = occupancy_of<true, RT_DF_BATCH>(&per_cu);
         else if (v == (RT_DF_BATCH | RT_V_FAN)) e = occupancy_of<true, RT_DF_BATCH | RT_V_FAN>(&per_cu);
         else if (v == RT_DF_FRAME) e = occupancy_of<true, RT_DF_FRAME>(&per_cu);
-        else if (v == RT_DF_ALT1) e = occupancy_of<true, RT_DF_ALT1>(&per_cu);
-        else e = occupancy_of<true, RT_DF_ALT2>(&per_cu);
+        else e = occupancy_of<true, RT_DF_ALT>(&per_cu);
     } else {
-        if (v == RT_WT_DEFAULT) e = occupancy_of<false, RT_WT_DEFAULT>(&per_cu);
-        else e = occupancy_of<false, RT_WT_ALT1>(&per_cu);
+        e = occupancy_of<false, RT_WT_DEFAULT>(&per_cu);
     }
     if (e != 0 || per_cu <= 0) per_cu = 8;
     c->persistent_blocks[key] = std::max(1, cus) * per_cu;

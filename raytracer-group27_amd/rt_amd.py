@@ -154,10 +154,11 @@ OPT_KERNEL, OPT_COOP, OPT_COOP_MAX, OPT_REFILL, OPT_WAVE_TRACE, OPT_VARIANT, OPT
 OPT_DUAL_STEP = 10
 KERNEL_AUTO, KERNEL_WHOLE_TRAVERSAL, KERNEL_DYNAMIC_FETCH = 0, 1, 2
 # compiled kernel variants (rt_megakernel.hip RT_V_*, rt_runtime.hip RT_DF_* / RT_WT_*)
-V_CALL, V_NOPF, V_NOCOOP, V_W3, V_W4, V_W5 = 1, 2, 4, 8, 16, 128
+V_CALL, V_NOPF, V_NOCOOP, V_W4 = 1, 2, 4, 16
 DF_BATCH, DF_FRAME = V_CALL | V_NOPF | V_NOCOOP | V_W4, 0  # shipped dynamic-fetch variants (by render shape)
-DF_VARIANTS = [DF_BATCH, DF_FRAME, V_CALL | V_NOPF | V_NOCOOP | V_W3, V_CALL | V_NOPF | V_NOCOOP | V_W5]
-WT_VARIANTS = [0, V_CALL | V_W3]
+DF_ALT = V_CALL | V_NOPF | V_W4  # the one A/B alternate: the batch variant with out-of-line drain lane groups
+DF_VARIANTS = [DF_BATCH, DF_FRAME, DF_ALT]
+WT_VARIANTS = [0]
 
 class rt_post_params(C.Structure):
     """Screen post-processing settings (src/screen.h:58-111), raw setter values."""

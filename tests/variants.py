@@ -1,5 +1,6 @@
-"""Render-path selection for the bit-identity tests: every compiled kernel variant and drain /
-refill setting of both kernel classes (rt_ctx_set_option; the library reads no environment)."""
+"""Render-path selection for the bit-identity tests: every compiled kernel variant (the shipped ones and
+the one A/B alternate, DF_ALT: the out-of-line drain lane groups) and drain / refill setting of both kernel
+classes (rt_ctx_set_option; the library reads no environment)."""
 import contextlib
 
 
@@ -29,6 +30,7 @@ def all_variants(R):
         {R.OPT_KERNEL: wt, R.OPT_INTERLEAVE: 1},
         {R.OPT_KERNEL: df, R.OPT_DUAL_STEP: 0},                 # one record or one node visit per step
         {R.OPT_KERNEL: df, R.OPT_VARIANT: R.DF_BATCH, R.OPT_DUAL_STEP: 0},
+        {R.OPT_KERNEL: df, R.OPT_VARIANT: R.DF_ALT, R.OPT_COOP: 2, R.OPT_REFILL: 64},  # out-of-line drain, steady state
     ]
     return out
 
