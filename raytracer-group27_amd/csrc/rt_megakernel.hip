@@ -759,21 +759,22 @@ __device__ __forceinline__ void new_tree(Lane& L) {
     L.sdist = 0.0f;
 }
 
-// queue the camera ray of the lane's current sample (src/main.cpp:350-386)
-__device__ __forceinline__ void queue_camera(const KParams& P, Lane& L, Query& q) {
-    const int py = (int)(L.rpix / (uint32_t)P.W);
-    const int px = (int)(L.rpix - (uint32_t)py * (uint32_t)P.W);
+// the camera ray of pixel rpix's camera sample `sample` (src/main.cpp:350-386); job = the pixel's job
+// (its view in a batch)
+__device__ __forceinline__ void camera_query(const KParams& P, int job, uint32_t rpix, int sample, Query& q) {
+    const int py = (int)(rpix / (uint32_t)P.W);
+    const int px = (int)(rpix - (uint32_t)py * (uint32_t)P.W);
     const float ndx = (float)px / (float)P.W * 2.0f - 1.0f;
     const float ndy = (float)py / (float)P.H * 2.0f - 1.0f;
     float sx = ndx, sy = ndy;
     if (P.aa) {
-        const int s = L.sample;
+        const int s = sample;
         sx = (s == 0 || s == 2) ? ndx - P.aa_offx : ndx + P.aa_offx;
         sy = (s < 2) ? ndy + P.aa_offy : ndy - P.aa_offy;
     } else if (P.multi) {
         const int per_q = ((P.ms_moves + 1) / 2) * ((P.ms_moves + 1) / 2);
-        const int qd = L.sample / per_q;
-        const int r = L.sample % per_q;
+        const int qd = sample / per_q;
+        const int r = sample % per_q;
         const int nyv = (P.ms_moves + 1) / 2;
         const int xx = 1 + 2 * (r / nyv);
         const int yy = 1 + 2 * (r % nyv);
@@ -784,11 +785,16 @@ __device__ __forceinline__ void queue_camera(const KParams& P, Lane& L, Query& q
     }
     if (P.n_views > 1) {
         int view;
-        view_job(P, L.job, view);
+        view_job(P, job, view);
         gen_ray_view(P, view, sx, sy, q.o, q.d);
     } else
         gen_ray(P, sx, sy, q.o, q.d);
     q.t = FLT_MAX;
+}
+
+// queue the camera ray of the lane's current sample
+__device__ __forceinline__ void queue_camera(const KParams& P, Lane& L, Query& q) {
+    camera_query(P, L.job, L.rpix, L.sample, q);
     new_tree(L);
 }
 
@@ -875,6 +881,28 @@ __device__ __attribute__((noinline)) int cansee_step_call(const void* ka, Query&
     return cansee_step(kernel_params(ka).S, q, hit, b, sI, sdist);
 }
 
+// A camera sample of pixel job `job` is complete with colour acc: the pixel's samples are summed in its
+// output slot in sample order (setPixel of the average, src/main.cpp:358-395).  True if the pixel has
+// more samples.
+__device__ __forceinline__ bool store_sample(const KParams& P, int job, int sample, v3 acc) {
+    uint32_t rpix;
+    int out_row;
+    job_pixel(P, job, rpix, out_row);
+    const int px = (int)(rpix % (uint32_t)P.W);
+    float* dst = P.out + ((size_t)out_row * P.W + px) * 3;
+    const int nsamples = P.aa ? 4 : (P.multi ? P.sample_size : 1);
+    v3 col = acc;
+    if (nsamples > 1) {
+        const v3 sum = (sample == 0) ? v3{0.0f, 0.0f, 0.0f} : v3{dst[0], dst[1], dst[2]};
+        col = sum + acc;
+        if (sample + 1 == nsamples) col = P.aa ? col * 0.25f : col * (float)(1.0f / (float)P.sample_size);
+    }
+    dst[0] = col.x;
+    dst[1] = col.y;
+    dst[2] = col.z;
+    return sample + 1 < nsamples;
+}
+
 // The state-machine advance after a finished query (q = that query's ray; hit, b = its result):
 // the cansee segment loop, the light loop, the recursion tree, the camera samples and the pixel
 // output.  Returns true with the next query in q (L.shadow says which kind); false when the lane's
@@ -916,23 +944,8 @@ __device__ __forceinline__ bool advance_lane(const KParams& P, const JobSrc& J, 
     if (more) return true;
     // camera sample complete: the pixel's samples are summed in its output slot, in sample order
     if (J.mode == 0) {
-        uint32_t rpix;
-        int out_row;
-        job_pixel(P, L.job, rpix, out_row);
-        const int px = (int)(rpix % (uint32_t)P.W);
-        float* dst = P.out + ((size_t)out_row * P.W + px) * 3;
-        const int nsamples = P.aa ? 4 : (P.multi ? P.sample_size : 1);
-        v3 col = L.acc;
-        if (nsamples > 1) {
-            const v3 sum = (L.sample == 0) ? v3{0.0f, 0.0f, 0.0f} : v3{dst[0], dst[1], dst[2]};
-            col = sum + L.acc;
-            if (L.sample + 1 == nsamples) col = P.aa ? col * 0.25f : col * (float)(1.0f / (float)P.sample_size);
-        }
-        dst[0] = col.x;
-        dst[1] = col.y;
-        dst[2] = col.z;
-        L.sample++;
-        if (L.sample < nsamples) {
+        if (store_sample(P, L.job, L.sample, L.acc)) {
+            L.sample++;
             queue_camera(P, L, q);
             return true;
         }
@@ -963,6 +976,7 @@ __device__ __attribute__((noinline)) bool advance_lane_call(const void* ka, Lane
 #define RT_V_NOCOOP 4
 #define RT_V_W4 16  // compiled for 4 waves per SIMD (128 VGPRs)
 #define RT_V_FAN 256  // dynamic fetch: the spherical-light sample fans compiled in (P.fan)
+
 #define RT_V_WAVES(V) (((V) & RT_V_W4) ? 4 : 2)
 
 
@@ -1936,6 +1950,289 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
         w[5] = lanes_drain;
         w[6] = coop_n;
         w[7] = pa_drain;
+    }
+}
+
+// ---- the opaque-scene kernel: point and spot lights, mirror recursion --------------------------
+// getFinalColor (src/main.cpp:129-301) on a scene whose materials are all opaque (transparency == 1),
+// lit only by point and spot lights (src/shadow.cpp:106-131,229-252), without glossy lobes
+// (glossy_ray_count == 1) or textures: every node has at most one child (the ks^2-weighted mirror ray)
+// and every shadow query is an any-hit cansee of one segment.  The recursion tree is then a chain, the
+// light loop a cursor over the point then the spot lights, and the whole per-lane state -- pixel, camera
+// sample, recursion level, colour and weights, the shading point -- is 24 dwords that stay in registers:
+// the state machine runs inline between traversal steps, with no private-memory frame and no call.
+// Its arithmetic is the general state machine's (begin_node, advance_lights_body, the forward colour
+// fold), so the image and the ray count are bit-identical (tests/test_gpu_parity.py variant matrix).
+struct LiteLane {
+    int job;        // >= 0 job; -1 idle (fetch another); -2 no more work
+    uint32_t rpix;  // the reference's pixel id y * W + x
+    uint32_t sample : 7;  // camera sample
+    uint32_t level : 5;   // recursion level of the current node
+    uint32_t desc : 1;    // the current node descends to its mirror child after its lights
+    uint32_t shadow : 1;  // the query in flight is a cansee segment
+    uint32_t li : 18;     // light cursor: point lights [0, npl), then spot lights
+    v3 acc, w, wc;        // sample colour, weight of the current node, of its mirror child
+    v3 hp, nN, refl;      // shading point, normalize(normal), reflect
+    int mat;              // >= 0 mesh material, < 0 sphere -(s+1)
+    v3 color;             // direct light of the current node
+};
+
+// The next light of the cursor that needs a cansee segment (true, query in q, cursor on it), or false
+// when the node's lights are done.  Lights whose target lies within SHADOW_ERROR_OFFSET are visible
+// without a query (src/shadow.cpp:38-40) and spot lights outside their cone contribute nothing
+// (src/shadow.cpp:235-237).
+template <bool COUNT>
+__device__ __forceinline__ bool lite_next_light(const KParams& P, LiteLane& L, Query& q, float& sdist) {
+    const DevScene& S = P.S;
+    const int nl = S.npl + S.nspot;
+    while ((int)L.li < nl) {
+        v3 lp, lc;
+        if ((int)L.li < S.npl) {
+            const rt_point_light pl = S.pl[L.li];
+            lp = ld3(pl.position);
+            lc = ld3(pl.color);
+        } else {
+            const DSpot sp = S.spot[L.li - S.npl];
+            lp = ld3(sp.pos);
+            lc = ld3(sp.color);
+            if (!(dot(normalize(ld3(sp.dir)), normalize(L.hp - lp)) > sp.cos_angle)) {
+                L.li++;
+                continue;
+            }
+        }
+        v3 d = lp - L.hp;  // start_cansee
+        sdist = length(d);
+        d = normalize(d);
+        if (sdist > 0.0005f) {
+            q.o = L.hp + 0.0005f * d;
+            q.d = d;
+            q.t = FLT_MAX;
+            return true;
+        }
+        // visible without a query (cansee's loop condition fails at once): the light counts at once
+        const v3 ldir = normalize(lp - L.hp);
+        const float cosL = fabsf(dot(L.nN, ldir));
+        const float d2 = dot(normalize(L.refl), ldir);
+        L.color += calc_color(lc, 1.0f, cosL, (0.0f < d2) ? d2 : 0.0f, load_mat(S, L.mat));
+        L.li++;
+    }
+    return false;
+}
+
+// the light under the cursor was visible: its calcColor into the node's colour
+__device__ __forceinline__ void lite_light_visible(const KParams& P, LiteLane& L) {
+    const DevScene& S = P.S;
+    v3 lp, lc;
+    if ((int)L.li < S.npl) {
+        const rt_point_light pl = S.pl[L.li];
+        lp = ld3(pl.position);
+        lc = ld3(pl.color);
+    } else {
+        const DSpot sp = S.spot[L.li - S.npl];
+        lp = ld3(sp.pos);
+        lc = ld3(sp.color);
+    }
+    const v3 ldir = normalize(lp - L.hp);
+    const float cosL = fabsf(dot(L.nN, ldir));
+    const float d2 = dot(normalize(L.refl), ldir);
+    L.color += calc_color(lc, 1.0f, cosL, (0.0f < d2) ? d2 : 0.0f, load_mat(S, L.mat));
+}
+
+// The state-machine advance of the opaque-scene kernel after a finished query (q = its ray, hit / b =
+// its result): true with the next query in q (sdist: its cansee distance), false when the job is done.
+template <bool COUNT>
+__device__ __forceinline__ bool lite_advance(const KParams& P, LiteLane& L, bool hit, const Best& b, Query& q,
+                                             float& sdist, Cnt& cnt) {
+    const DevScene& S = P.S;
+    bool node_done;
+    if (L.shadow) {
+        // cansee in an opaque scene: visible iff no candidate at t <= distance - 2 * SHADOW_ERROR_OFFSET
+        if (!hit) lite_light_visible(P, L);
+        L.li++;
+        L.shadow = false;
+        node_done = true;
+    } else if (hit) {
+        // begin_node (src/main.cpp:131-256), the opaque branch
+        const Surf s = surface(S, q.o, q.d, b, false, L.level == 0);
+        if (COUNT) {
+            cnt.hits++;
+            if (s.ub) cnt.ub++;
+        }
+        L.hp = s.p;
+        L.nN = normalize(s.n);
+        L.refl = reflect(normalize(q.d), L.nN);
+        L.mat = (b.rec >= 0) ? s.mesh : b.rec;
+        L.color = v3{0.0f, 0.0f, 0.0f};
+        L.li = 0;
+        L.desc = false;
+        if (L.level < P.max_level) {
+            const v3 ks{s.m.ks[0], s.m.ks[1], s.m.ks[2]};
+            if (ks.x > 0.0f || ks.y > 0.0f || ks.z > 0.0f) {
+                L.desc = true;
+                // color += ks * reflectColor (/ glossy_ray_count with shininess): the child's weight
+                L.wc = (s.m.shin != 0.0f) ? L.w * ((ks * ks) / (float)P.glossy_n) : L.w * (ks * ks);
+            }
+        }
+        node_done = true;
+    } else {
+        node_done = false;  // a miss: getFinalColor returns black, the camera sample is complete
+    }
+    if (node_done) {
+        if (lite_next_light<COUNT>(P, L, q, sdist)) {
+            L.shadow = true;
+            return true;
+        }
+        L.acc = L.acc + L.w * L.color;  // every light done: the node's colour, then its mirror child
+        if (L.desc) {
+            L.w = L.wc;
+            L.level++;
+            q.o = L.hp + 0.01f * L.refl;
+            q.d = L.refl;
+            q.t = FLT_MAX;
+            return true;
+        }
+    }
+    // camera sample complete
+    if (store_sample(P, L.job, L.sample, L.acc)) {
+        L.sample++;
+        camera_query(P, L.job, L.rpix, L.sample, q);
+        L.acc = v3{0.0f, 0.0f, 0.0f};
+        L.w = v3{1.0f, 1.0f, 1.0f};
+        L.level = 0;
+        L.desc = false;
+        L.shadow = false;
+        return true;
+    }
+    L.job = -1;
+    return false;
+}
+
+template <bool COUNT, int V>
+__global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KParams P, JobSrc J) {
+    constexpr bool PF = !(V & RT_V_NOPF);
+    __shared__ int stack_lds[RT_STACK8 * RT_WAVE];
+    __shared__ int s_base, s_lim;
+    const int lane_id = threadIdx.x;
+    int* stk = stack_lds + lane_id;
+    const unsigned long long t_wave0 = P.wave_trace ? wall_clock64() : 0ull;
+    unsigned int wave_jobs = 0;
+    const DevScene& S = P.S;
+    LiteLane L;
+    L.job = -1;
+    L.shadow = false;
+    Trav T;
+    Cnt cnt{};
+    int xr = (int)(blockIdx.x & 7), xtried = 0;
+    bool tracing = false, pending = false;
+    const int refill_at = P.refill;
+    unsigned long long t_exh = 0ull;
+    for (;;) {
+        // ---- phase A: advance the pending lanes, then refill the idle ones ----
+        unsigned long long tA = COUNT ? (unsigned long long)clock64() : 0ull;
+        bool start = false;
+        Query q;
+        float qsdist = 0.0f;
+        if (pending) {
+            pending = false;
+            if (COUNT && wave_leader()) cnt.wadv++;
+            q.o = T.o;
+            q.d = T.d;
+            const int jb = L.job;
+            start = lite_advance<COUNT>(P, L, T.found, T.best, q, qsdist, cnt);
+            if (P.job_trace && L.job == -1) P.job_trace[3 * jb + 1] = wall_clock64();
+        }
+        const unsigned long long tJ = COUNT ? (unsigned long long)clock64() : 0ull;
+        if (COUNT) cnt.cyc_c += tJ - tA;
+        const bool idle = (L.job == -1) && !start && !tracing;
+        const unsigned long long want = __ballot(idle);
+        if (want) {
+            const int nwant = __popcll(want);
+            if (lane_id == __ffsll((long long)want) - 1) {
+                const int lo = xq_lo(J, xr);
+                s_base = lo + atomicAdd(J.xq + 32 * xr, nwant);
+                s_lim = xr == 7 ? J.njobs : xq_lo(J, xr + 1);
+            }
+            wave_jobs += (unsigned int)nwant;
+            __builtin_amdgcn_wave_barrier();
+            __syncthreads();
+            const int base = s_base, lim = s_lim;
+            if (base + nwant >= lim) {  // this group's range is used up: go on to the next
+                xr = (xr + 1) & 7;
+                ++xtried;
+            }
+            if (idle) {
+                const int job_k = base + __popcll(want & ((1ull << lane_id) - 1ull));
+                if (job_k < lim) {
+                    if (P.job_trace) P.job_trace[3 * job_k] = wall_clock64();
+                    int out_row;
+                    L.job = job_k;
+                    if (job_pixel(P, job_k, L.rpix, out_row)) {
+                        L.sample = 0;
+                        camera_query(P, job_k, L.rpix, 0, q);
+                        L.acc = v3{0.0f, 0.0f, 0.0f};
+                        L.w = v3{1.0f, 1.0f, 1.0f};
+                        L.level = 0;
+                        L.desc = false;
+                        L.shadow = false;
+                        qsdist = 0.0f;
+                        start = true;
+                    } else {
+                        L.job = -1;  // a padding pixel
+                    }
+                } else {
+                    L.job = xtried < 8 ? -1 : -2;
+                }
+            }
+            __syncthreads();
+        }
+        if (COUNT) cnt.cyc_d += (unsigned long long)clock64() - tJ;
+        if (start) {
+            cnt.rays++;
+            trav_init_q(S, P.use_bvh != 0, q.o, q.d, q.t, L.shadow, qsdist, T);
+            tracing = true;
+        }
+        if (P.wave_trace && !t_exh && __any(L.job == -2)) t_exh = wall_clock64();
+        if (!__any(tracing)) {
+            if (!__any(L.job == -1 || pending)) break;  // every lane exhausted
+            continue;
+        }
+        // ---- phase B: one node visit and / or one leaf record per lane and iteration ----
+        unsigned long long tB = 0ull;
+        if (COUNT) {
+            tB = (unsigned long long)clock64();
+            cnt.cyc_a += tB - tA;
+        }
+        float4 g[8];
+        if (PF && tracing && T.cur != RT_TRAV_NONE) node_fetch(S.nodes, T.cur, g);
+        for (;;) {
+            if (COUNT) {
+                const int ntr = __popcll(__ballot(tracing));
+                if (wave_leader()) cnt.hist[min((ntr - 1) >> 4, 2)]++;
+            }
+            if (tracing) {
+                const bool rec = leaf_pending(T);
+                if (rec) trav_record<COUNT, true>(S, T, cnt);
+                const bool nv = T.cur != RT_TRAV_NONE && (!rec || (P.dual && T.lh == 0u));
+                if (nv) trav_node<COUNT, 8, PF>(S, T, stk, g, cnt);
+            }
+            if (tracing && !leaf_pending(T) && T.cur == RT_TRAV_NONE) {
+                trav_finish(S, T);
+                tracing = false;
+                pending = true;
+            }
+            if (!__any(tracing)) break;
+            if (__popcll(__ballot(pending || L.job == -1)) >= refill_at) break;
+        }
+        if (COUNT) cnt.cyc_b += (unsigned long long)clock64() - tB;
+    }
+    flush_counters<COUNT>(P, cnt);
+    if (P.wave_trace && lane_id == 0) {
+        unsigned long long* w = P.wave_trace + 8 * blockIdx.x;
+        w[0] = t_wave0;
+        w[1] = wall_clock64();
+        w[2] = wave_jobs;
+        w[3] = t_exh;
+        for (int k = 4; k < 8; ++k) w[k] = 0ull;
     }
 }
 

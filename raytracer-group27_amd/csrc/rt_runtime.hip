@@ -104,6 +104,7 @@ struct rt_ctx {
     bool df_ok = true;  // the BVH8 fits the dynamic-fetch kernel's LDS stack
     bool glossy_material = false;  // opaque, ks > 0, shininess != 0 (glossy_ray_count > 1 draws lobes)
     int persistent_blocks[1024] = {0};  // resident 64-lane blocks per (kernel class, variant)
+    int opaque_blocks[2] = {0, 0};      // ... of the opaque-scene kernel
     // lights (re-uploadable: rt_update_lights)
     void* d_lights[4] = {nullptr, nullptr, nullptr, nullptr};
     // developer wave trace (RT_OPT_WAVE_TRACE)
@@ -127,6 +128,7 @@ struct rt_ctx {
     int opt_fan_cap = 0;      // pixels a wave may have waiting on fans before it stops taking new ones (0: default)
     int opt_dual = -1;        // dynamic-fetch steps: record and node visit in one iteration (-1 default, 0 off, 1 on)
     int opt_variant = -1;   // -1: the shipped variant for the render shape (RT_DF_BATCH / _FRAME, RT_WT_DEFAULT)
+    int opt_opaque = -1;    // opaque-scene kernel: -1 where eligible, 0 never (general kernels), 2 its no-prefetch A/B build
     char last_kernel[64] = {0};
     // view batches: the camera table's pinned host staging and the event of its last copy (the buffer
     // is refilled only once that copy has read it)
@@ -820,6 +822,10 @@ static int set_option_one(rt_ctx* c, int option, int value) {
             if (value < -1 || value > 511) break;
             c->opt_variant = value;
             return RT_OK;
+        case RT_OPT_OPAQUE:
+            if (value < -1 || value > 2) break;
+            c->opt_opaque = value;
+            return RT_OK;
         default:
             set_error("rt_ctx_set_option: unknown option");
             return RT_ERR_INVALID;
@@ -871,6 +877,19 @@ static bool use_df(const rt_ctx* c, const KParams& K) {
 #define RT_WT_DEFAULT 0
 // the one A/B alternate: the batch variant with the drain lane groups, called out of line
 #define RT_DF_ALT (RT_V_CALL | RT_V_NOPF | RT_V_W4)
+// the opaque-scene kernel (rt_megakernel.hip persistent_opaque_kernel): 4 waves per SIMD
+#define RT_OPAQUE_V (RT_V_W4)
+#define RT_OPAQUE_V2 (RT_V_W4 | RT_V_NOPF)
+
+// Renders that the opaque-scene kernel draws: pixels (not rt_shade's explicit rays) of a large scene
+// (the dynamic-fetch class) whose materials are all opaque, lit by point and spot lights only, without
+// textures and without glossy lobes (glossy_ray_count 1, or no glossy material).  RT_OPT_OPAQUE 0 and any
+// RT_OPT_VARIANT choice select the general kernels instead.
+static bool use_df(const rt_ctx* c, const KParams& K);
+static bool opaque_path(const rt_ctx* c, const KParams& K, bool pixels) {
+    return pixels && c->opt_opaque != 0 && c->opt_variant < 0 && use_df(c, K) && K.S.all_opaque && K.S.nsl == 0 &&
+           K.S.nplane == 0 && !K.S.tex_on && (K.glossy_n == 1 || !c->glossy_material);
+}
 
 // by render shape: view batches and sample-fan renders run the lean 4-wave variant (C4 single frame
 // with fans: 27.1 vs 30.3 ms), other single frames the 2-wave variant with the drain lane groups
@@ -901,6 +920,15 @@ static bool launch_shipped(bool df, int v, int grid, hipStream_t st, const KPara
 
 template <bool COUNT>
 static int launch_persistent(int grid, hipStream_t st, const KParams& K, const JobSrc& J, rt_ctx* c) {
+    if (opaque_path(c, K, J.mode == 0)) {
+        if (c->opt_opaque == 2)
+            hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V2>), dim3(grid), dim3(64), 0, st, K, J);
+        else
+            hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V>), dim3(grid), dim3(64), 0, st, K, J);
+        std::snprintf(c->last_kernel, sizeof(c->last_kernel), "rt::persistent_opaque_kernel<%s, %d>",
+                      COUNT ? "true" : "false", c->opt_opaque == 2 ? RT_OPAQUE_V2 : RT_OPAQUE_V);
+        return RT_OK;
+    }
     const bool df = use_df(c, K);
     const bool tex = COUNT || K.S.tex_on;  // counting builds keep the texture code (one instance each)
     const int v = variant_of(c, df, K);
@@ -930,7 +958,19 @@ static int occupancy_of(int* per_cu) {
 }
 
 // resident 64-lane blocks of the kernel (the persistent grid)
-static int persistent_grid(rt_ctx* c, const KParams& K) {
+static int persistent_grid(rt_ctx* c, const KParams& K, bool pixels) {
+    if (opaque_path(c, K, pixels)) {
+        const int key = c->opt_opaque == 2 ? 1 : 0;
+        if (c->opaque_blocks[key] > 0) return c->opaque_blocks[key];
+        int cus = 0, per_cu = 0;
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
+        const hipError_t e =
+            key ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V2>, 64, 0)
+                : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V>, 64, 0);
+        if (e != hipSuccess || per_cu <= 0) per_cu = 8;
+        c->opaque_blocks[key] = std::max(1, cus) * per_cu;
+        return c->opaque_blocks[key];
+    }
     const bool df = use_df(c, K);
     const int v = variant_of(c, df, K);
     const int key = (df ? 512 : 0) + (v & 511);
@@ -1113,7 +1153,7 @@ static int launch_render(rt_ctx* c, KParams& K, hipStream_t st, int count_mode, 
         K.view_jobs = J.view_jobs;
         J.counter = reinterpret_cast<int*>(c->d_stats + 7);
         J.xq = use_df(c, K) ? reinterpret_cast<int*>(c->d_stats + 16) : nullptr;
-        const int grid = (int)std::min<long long>(blocks * J.n_views, persistent_grid(c, K));
+        const int grid = (int)std::min<long long>(blocks * J.n_views, persistent_grid(c, K, true));
         if (c->opt_wave_trace) {
             const int rc = ensure(c, &c->d_wave_trace, &c->wave_trace_bytes,
                                   (size_t)grid * 8 * 8 + (size_t)J.njobs * 3 * 8);
@@ -1464,7 +1504,7 @@ extern "C" int rt_shade(rt_ctx* c, const rt_ray* rays, int n, const rt_params* p
         J.view_jobs = n;
         J.counter = reinterpret_cast<int*>(c->d_stats + 7);
         J.xq = use_df(c, K) ? reinterpret_cast<int*>(c->d_stats + 16) : nullptr;
-        const int grid = std::min((n + 63) / 64, persistent_grid(c, K));
+        const int grid = std::min((n + 63) / 64, persistent_grid(c, K, false));
         const int lrc = g_count_mode ? launch_persistent<true>(grid, c->stream, K, J, c)
                                      : launch_persistent<false>(grid, c->stream, K, J, c);
         if (lrc != RT_OK) e = hipErrorInvalidValue;
