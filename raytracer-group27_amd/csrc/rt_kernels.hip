@@ -105,7 +105,6 @@ struct KParams {
     int interleave;             // job -> pixel: a wave's 64 jobs are one pixel of each of 64 tiles
     int fan_cap;                // ... a wave with this many pixels waiting on fans takes no new pixels
     int dual;                   // dynamic-fetch kernel: a lane testing a leaf's records also visits its next node
-    int ahead;                  // opaque-scene kernel: mirror-ahead (helper lanes trace a node's light segments)
     uint32_t seed_lo, seed_hi;  // glossy sampling: Philox-4x32-10 key (rt_params.rng_seed)
     unsigned long long* wave_trace;  // developer wave trace (rt_ctx_set_option RT_OPT_WAVE_TRACE), or null
     unsigned long long* job_trace;   // ... and per job: start, end (100 MHz clock), queries

@@ -1971,160 +1971,87 @@ struct LiteLane {
     uint32_t level : 5;   // recursion level of the current node
     uint32_t desc : 1;    // the current node descends to its mirror child after its lights
     uint32_t shadow : 1;  // the query in flight is a cansee segment
-    uint32_t ahead : 1;   // the query in flight is the mirror child, traced while helpers trace the lights
-    uint32_t li : 17;     // light cursor: point lights [0, npl), then spot lights
+    uint32_t li : 18;     // light cursor: point lights [0, npl), then spot lights
     v3 acc, w, wc;        // sample colour, weight of the current node, of its mirror child
     v3 hp, nN, refl;      // shading point, normalize(normal), reflect
     int mat;              // >= 0 mesh material, < 0 sphere -(s+1)
     v3 color;             // direct light of the current node
 };
 
-// Light li of the node at L.hp: its position and colour, and whether getPointLights / getSpotLichts
-// trace it (false: a spot light that does not face the point, src/shadow.cpp:235-237).
-__device__ __forceinline__ bool lite_light(const DevScene& S, const LiteLane& L, int li, v3& lp, v3& lc) {
-    if (li < S.npl) {
-        const rt_point_light pl = S.pl[li];
+// The next light of the cursor that needs a cansee segment (true, query in q, cursor on it), or false
+// when the node's lights are done.  Lights whose target lies within SHADOW_ERROR_OFFSET are visible
+// without a query (src/shadow.cpp:38-40) and spot lights outside their cone contribute nothing
+// (src/shadow.cpp:235-237).
+template <bool COUNT>
+__device__ __forceinline__ bool lite_next_light(const KParams& P, LiteLane& L, Query& q, float& sdist) {
+    const DevScene& S = P.S;
+    const int nl = S.npl + S.nspot;
+    while ((int)L.li < nl) {
+        v3 lp, lc;
+        if ((int)L.li < S.npl) {
+            const rt_point_light pl = S.pl[L.li];
+            lp = ld3(pl.position);
+            lc = ld3(pl.color);
+        } else {
+            const DSpot sp = S.spot[L.li - S.npl];
+            lp = ld3(sp.pos);
+            lc = ld3(sp.color);
+            if (!(dot(normalize(ld3(sp.dir)), normalize(L.hp - lp)) > sp.cos_angle)) {
+                L.li++;
+                continue;
+            }
+        }
+        v3 d = lp - L.hp;  // start_cansee
+        sdist = length(d);
+        d = normalize(d);
+        if (sdist > 0.0005f) {
+            q.o = L.hp + 0.0005f * d;
+            q.d = d;
+            q.t = FLT_MAX;
+            return true;
+        }
+        // visible without a query (cansee's loop condition fails at once): the light counts at once
+        const v3 ldir = normalize(lp - L.hp);
+        const float cosL = fabsf(dot(L.nN, ldir));
+        const float d2 = dot(normalize(L.refl), ldir);
+        L.color += calc_color(lc, 1.0f, cosL, (0.0f < d2) ? d2 : 0.0f, load_mat(S, L.mat));
+        L.li++;
+    }
+    return false;
+}
+
+// the light under the cursor was visible: its calcColor into the node's colour
+__device__ __forceinline__ void lite_light_visible(const KParams& P, LiteLane& L) {
+    const DevScene& S = P.S;
+    v3 lp, lc;
+    if ((int)L.li < S.npl) {
+        const rt_point_light pl = S.pl[L.li];
         lp = ld3(pl.position);
         lc = ld3(pl.color);
-        return true;
+    } else {
+        const DSpot sp = S.spot[L.li - S.npl];
+        lp = ld3(sp.pos);
+        lc = ld3(sp.color);
     }
-    const DSpot sp = S.spot[li - S.npl];
-    lp = ld3(sp.pos);
-    lc = ld3(sp.color);
-    return dot(normalize(ld3(sp.dir)), normalize(L.hp - lp)) > sp.cos_angle;
-}
-
-// cansee(hp, lp)'s first segment (src/shadow.cpp:32-40): false when the loop condition fails at once
-// (the light is visible without a query)
-__device__ __forceinline__ bool lite_cansee_query(const LiteLane& L, v3 lp, Query& q, float& sdist) {
-    v3 d = lp - L.hp;
-    sdist = length(d);
-    d = normalize(d);
-    if (!(sdist > 0.0005f)) return false;
-    q.o = L.hp + 0.0005f * d;
-    q.d = d;
-    q.t = FLT_MAX;
-    return true;
-}
-
-// a visible light's calcColor into the node's colour (intensity 1: nothing transparent attenuates it)
-__device__ __forceinline__ void lite_add_light(const DevScene& S, LiteLane& L, v3 lp, v3 lc) {
     const v3 ldir = normalize(lp - L.hp);
     const float cosL = fabsf(dot(L.nN, ldir));
     const float d2 = dot(normalize(L.refl), ldir);
     L.color += calc_color(lc, 1.0f, cosL, (0.0f < d2) ? d2 : 0.0f, load_mat(S, L.mat));
 }
 
-// The next light of the cursor that needs a cansee segment (true, query in q, cursor on it), or false
-// when the node's lights are done; lights visible without a query count at once, in loop order.
-__device__ __forceinline__ bool lite_next_light(const KParams& P, LiteLane& L, Query& q, float& sdist) {
-    const DevScene& S = P.S;
-    const int nl = S.npl + S.nspot;
-    for (; (int)L.li < nl; L.li++) {
-        v3 lp, lc;
-        if (!lite_light(S, L, L.li, lp, lc)) continue;
-        if (lite_cansee_query(L, lp, q, sdist)) return true;
-        lite_add_light(S, L, lp, lc);
-    }
-    return false;
-}
-
-// the cansee segments the node's light loop traces (mirror-ahead: one helper lane each)
-__device__ __forceinline__ int lite_count_queries(const KParams& P, const LiteLane& L) {
-    const DevScene& S = P.S;
-    const int nl = S.npl + S.nspot;
-    int n = 0;
-    for (int li = 0; li < nl; ++li) {
-        v3 lp, lc;
-        Query q;
-        float sd;
-        if (lite_light(S, L, li, lp, lc) && lite_cansee_query(L, lp, q, sd)) ++n;
-    }
-    return n;
-}
-
-// the whole light loop of the node replayed in order with the helpers' visibility bits (bit k = the k-th
-// traced segment visible): the same additions as the loop that traces them one by one
-__device__ __forceinline__ void lite_replay_lights(const KParams& P, LiteLane& L, uint32_t vis) {
-    const DevScene& S = P.S;
-    const int nl = S.npl + S.nspot;
-    int k = 0;
-    for (int li = 0; li < nl; ++li) {
-        v3 lp, lc;
-        Query q;
-        float sd;
-        if (!lite_light(S, L, li, lp, lc)) continue;
-        if (lite_cansee_query(L, lp, q, sd)) {
-            if (!((vis >> k++) & 1u)) continue;
-        }
-        lite_add_light(S, L, lp, lc);
-    }
-}
-
-// the camera sample is complete: store it; true with the pixel's next sample queued in q
-__device__ __forceinline__ bool lite_sample_done(const KParams& P, LiteLane& L, Query& q) {
-    if (store_sample(P, L.job, L.sample, L.acc)) {
-        L.sample++;
-        camera_query(P, L.job, L.rpix, L.sample, q);
-        L.acc = v3{0.0f, 0.0f, 0.0f};
-        L.w = v3{1.0f, 1.0f, 1.0f};
-        L.level = 0;
-        L.desc = false;
-        L.shadow = false;
-        return true;
-    }
-    L.job = -1;
-    return false;
-}
-
-// the node's light loop from the cursor, one segment at a time: the next light's segment, or (every light
-// done) the node's colour folded and its mirror child queued, or the sample's end
-__device__ __forceinline__ bool lite_lights_seq(const KParams& P, LiteLane& L, Query& q, float& sdist) {
-    if (lite_next_light(P, L, q, sdist)) {
-        L.shadow = true;
-        return true;
-    }
-    L.acc = L.acc + L.w * L.color;  // every light done: the node's colour, then its mirror child
-    if (L.desc) {
-        L.w = L.wc;
-        L.level++;
-        q.o = L.hp + 0.01f * L.refl;
-        q.d = L.refl;
-        q.t = FLT_MAX;
-        return true;
-    }
-    return lite_sample_done(P, L, q);
-}
-
-enum { LITE_DONE = 0, LITE_QUERY = 1, LITE_AHEAD = 2 };
-
 // The state-machine advance of the opaque-scene kernel after a finished query (q = its ray, hit / b =
-// its result).  LITE_QUERY: the next query is in q (sdist: its cansee distance); LITE_DONE: the job is
-// complete; LITE_AHEAD (only with ahead_ok): a node was just begun whose mirror child exists and whose
-// lights need nq cansee segments -- the kernel may trace the child now and hand the segments to helper
-// lanes (mirror-ahead), or call lite_lights_seq for the loop's own order.  vis: an ahead node's helper
-// results, when the mirror child traced ahead is the query that finished.
+// its result): true with the next query in q (sdist: its cansee distance), false when the job is done.
 template <bool COUNT>
-__device__ __forceinline__ int lite_advance(const KParams& P, LiteLane& L, bool hit, const Best& b, Query& q,
-                                            float& sdist, Cnt& cnt, bool ahead_ok, uint32_t vis, int& nq) {
+__device__ __forceinline__ bool lite_advance(const KParams& P, LiteLane& L, bool hit, const Best& b, Query& q,
+                                             float& sdist, Cnt& cnt) {
     const DevScene& S = P.S;
-    if (L.ahead) {
-        // the parent's lights from its helpers, its colour, then the child -- the loop's order
-        L.ahead = false;
-        lite_replay_lights(P, L, vis);
-        L.acc = L.acc + L.w * L.color;
-        L.w = L.wc;
-        L.level++;
-    }
+    bool node_done;
     if (L.shadow) {
         // cansee in an opaque scene: visible iff no candidate at t <= distance - 2 * SHADOW_ERROR_OFFSET
-        if (!hit) {
-            v3 lp, lc;
-            lite_light(S, L, L.li, lp, lc);
-            lite_add_light(S, L, lp, lc);
-        }
+        if (!hit) lite_light_visible(P, L);
         L.li++;
         L.shadow = false;
+        node_done = true;
     } else if (hit) {
         // begin_node (src/main.cpp:131-256), the opaque branch
         const Surf s = surface(S, q.o, q.d, b, false, L.level == 0);
@@ -2147,37 +2074,48 @@ __device__ __forceinline__ int lite_advance(const KParams& P, LiteLane& L, bool 
                 L.wc = (s.m.shin != 0.0f) ? L.w * ((ks * ks) / (float)P.glossy_n) : L.w * (ks * ks);
             }
         }
-        if (ahead_ok && L.desc) {
-            nq = lite_count_queries(P, L);
-            if (nq > 0 && nq <= 32) return LITE_AHEAD;
-        }
+        node_done = true;
     } else {
-        // a miss: getFinalColor returns black, the camera sample is complete
-        return lite_sample_done(P, L, q) ? LITE_QUERY : LITE_DONE;
+        node_done = false;  // a miss: getFinalColor returns black, the camera sample is complete
     }
-    return lite_lights_seq(P, L, q, sdist) ? LITE_QUERY : LITE_DONE;
+    if (node_done) {
+        if (lite_next_light<COUNT>(P, L, q, sdist)) {
+            L.shadow = true;
+            return true;
+        }
+        L.acc = L.acc + L.w * L.color;  // every light done: the node's colour, then its mirror child
+        if (L.desc) {
+            L.w = L.wc;
+            L.level++;
+            q.o = L.hp + 0.01f * L.refl;
+            q.d = L.refl;
+            q.t = FLT_MAX;
+            return true;
+        }
+    }
+    // camera sample complete
+    if (store_sample(P, L.job, L.sample, L.acc)) {
+        L.sample++;
+        camera_query(P, L.job, L.rpix, L.sample, q);
+        L.acc = v3{0.0f, 0.0f, 0.0f};
+        L.w = v3{1.0f, 1.0f, 1.0f};
+        L.level = 0;
+        L.desc = false;
+        L.shadow = false;
+        return true;
+    }
+    L.job = -1;
+    return false;
 }
 
 template <bool COUNT, int V>
 __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KParams P, JobSrc J) {
-    // mirror-ahead (AHEAD, with P.ahead): lanes out of pixels trace the light segments of a node while its
-    // owner traces the node's mirror child, so a pixel's chain of queries is about halved in the drain
-    constexpr bool PF = !(V & RT_V_NOPF), COOP = !(V & RT_V_NOCOOP), AHEAD = COOP;
+    constexpr bool PF = !(V & RT_V_NOPF), COOP = !(V & RT_V_NOCOOP);
     __shared__ int stack_lds[RT_STACK8 * RT_WAVE];
-    __shared__ int coop_pool[COOP_POOL];   // drain lane groups (COOP): node groups of the wave's last queries;
-                                           // in phase A the mirror-ahead segment requests (9 words each)
+    __shared__ int coop_pool[COOP_POOL];   // drain lane groups (COOP): node groups of the wave's last queries
     __shared__ int coop_q[CQ_N * COOP_Q];  // ... and those queries
-    __shared__ int mb_req[RT_WAVE];        // mirror-ahead mailbox per owner lane: segments still traced,
-    __shared__ unsigned mb_vis[RT_WAVE];   // ... and their visibility bits
     __shared__ int s_base, s_lim;
     const int lane_id = threadIdx.x;
-    if (AHEAD) {
-        mb_req[lane_id] = 0;
-        mb_vis[lane_id] = 0u;
-        __syncthreads();
-    }
-    int help = -1, help_bit = 0;  // mirror-ahead helper: the owner lane and bit of the segment it traces
-    uint32_t job_q = 0;           // job trace: queries of the lane's pixel traced by the lane itself
     int* stk = stack_lds + lane_id;
     const unsigned long long t_wave0 = P.wave_trace ? wall_clock64() : 0ull;
     unsigned int wave_jobs = 0;
@@ -2185,7 +2123,6 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
     LiteLane L;
     L.job = -1;
     L.shadow = false;
-    L.ahead = false;
     Trav T;
     Cnt cnt{};
     int xr = (int)(blockIdx.x & 7), xtried = 0;
@@ -2195,103 +2132,17 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
     for (;;) {
         // ---- phase A: advance the pending lanes, then refill the idle ones ----
         unsigned long long tA = COUNT ? (unsigned long long)clock64() : 0ull;
-        bool start = false, qshadow = false;  // a new query, and whether it is a cansee segment
+        bool start = false;
         Query q;
         float qsdist = 0.0f;
-        if (AHEAD) {
-            // helpers whose segment finished: its visibility into the owner's mailbox (cansee in an opaque
-            // scene: visible iff no candidate), then the helper is free again
-            if (pending && help >= 0) {
-                pending = false;
-                if (!T.found) atomicOr(&mb_vis[help], 1u << help_bit);
-                atomicSub(&mb_req[help], 1);
-                help = -1;
-            }
-            __syncthreads();
-        }
-        int code = -1, nq = 0;  // this lane's lite_advance result this pass (-1: none)
-        // mirror-ahead only where the wave has lanes out of pixels (the drain; none in steady state)
-        const bool ahead_ok = AHEAD && P.ahead && __any(L.job == -2 && !tracing && !pending && help < 0);
-        // an owner whose mirror child finished waits for its helpers
-        if (pending && !(AHEAD && L.ahead && mb_req[lane_id] > 0)) {
+        if (pending) {
             pending = false;
             if (COUNT && wave_leader()) cnt.wadv++;
             q.o = T.o;
             q.d = T.d;
             const int jb = L.job;
-            code = lite_advance<COUNT>(P, L, T.found, T.best, q, qsdist, cnt, ahead_ok, AHEAD ? mb_vis[lane_id] : 0u,
-                                       nq);
-            start = code == LITE_QUERY;
-            qshadow = L.shadow;
-            if (P.job_trace && L.job == -1) {
-                P.job_trace[3 * jb + 1] = wall_clock64();
-                P.job_trace[3 * jb + 2] = job_q;
-            }
-        }
-        if (AHEAD && __any(code == LITE_AHEAD)) {
-            // nodes that may trace their mirror child ahead: each takes helpers for its nq segments from the
-            // lanes out of pixels, in lane order, while they last; the others run the loop one segment at a time
-            const bool cand = code == LITE_AHEAD;
-            const unsigned long long freel = __ballot(L.job == -2 && !tracing && !pending && help < 0);
-            const int nfree = __popcll(freel);
-            int inc = cand ? nq : 0;  // inclusive prefix of nq over the candidates
-            for (int off = 1; off < RT_WAVE; off <<= 1) {
-                const int u = __shfl_up(inc, off);
-                if (lane_id >= off) inc += u;
-            }
-            const int excl = inc - (cand ? nq : 0);
-            const bool take = cand && excl + nq <= nfree;  // (the taken candidates are a prefix: no gaps)
-            int nreq = take ? excl + nq : 0;
-            for (int off = RT_WAVE / 2; off > 0; off >>= 1) nreq = max(nreq, __shfl_xor(nreq, off));
-            if (take) {
-                const int nl = S.npl + S.nspot;
-                int k = 0;
-                for (int li = 0; li < nl; ++li) {
-                    v3 lp, lc;
-                    Query rq;
-                    float rsd;
-                    if (!lite_light(S, L, li, lp, lc) || !lite_cansee_query(L, lp, rq, rsd)) continue;
-                    int* r = coop_pool + 9 * (excl + k);
-                    r[0] = __float_as_int(rq.o.x);
-                    r[1] = __float_as_int(rq.o.y);
-                    r[2] = __float_as_int(rq.o.z);
-                    r[3] = __float_as_int(rq.d.x);
-                    r[4] = __float_as_int(rq.d.y);
-                    r[5] = __float_as_int(rq.d.z);
-                    r[6] = __float_as_int(rsd);
-                    r[7] = lane_id;
-                    r[8] = k++;
-                }
-                mb_req[lane_id] = nq;
-                mb_vis[lane_id] = 0u;
-                L.ahead = true;  // the mirror child now; the parent's lights are folded when it finishes
-                L.shadow = false;
-                q.o = L.hp + 0.01f * L.refl;
-                q.d = L.refl;
-                q.t = FLT_MAX;
-                qsdist = 0.0f;
-                start = true;
-                qshadow = false;
-            } else if (cand) {
-                start = lite_lights_seq(P, L, q, qsdist);
-                qshadow = L.shadow;
-            }
-            __syncthreads();
-            if ((freel >> lane_id) & 1ull) {
-                const int rank = __popcll(freel & ((1ull << lane_id) - 1ull));
-                if (rank < nreq) {
-                    const int* r = coop_pool + 9 * rank;
-                    q.o = v3{__int_as_float(r[0]), __int_as_float(r[1]), __int_as_float(r[2])};
-                    q.d = v3{__int_as_float(r[3]), __int_as_float(r[4]), __int_as_float(r[5])};
-                    q.t = FLT_MAX;
-                    qsdist = __int_as_float(r[6]);
-                    help = r[7];
-                    help_bit = r[8];
-                    start = true;
-                    qshadow = true;
-                }
-            }
-            __syncthreads();
+            start = lite_advance<COUNT>(P, L, T.found, T.best, q, qsdist, cnt);
+            if (P.job_trace && L.job == -1) P.job_trace[3 * jb + 1] = wall_clock64();
         }
         const unsigned long long tJ = COUNT ? (unsigned long long)clock64() : 0ull;
         if (COUNT) cnt.cyc_c += tJ - tA;
@@ -2326,11 +2177,8 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
                         L.level = 0;
                         L.desc = false;
                         L.shadow = false;
-                        L.ahead = false;
                         qsdist = 0.0f;
-                        qshadow = false;
                         start = true;
-                        job_q = 0;
                     } else {
                         L.job = -1;  // a padding pixel
                     }
@@ -2343,8 +2191,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
         if (COUNT) cnt.cyc_d += (unsigned long long)clock64() - tJ;
         if (start) {
             cnt.rays++;
-            if (P.job_trace) job_q = (help >= 0) ? job_q : job_q + 1;
-            trav_init_q(S, P.use_bvh != 0, q.o, q.d, q.t, qshadow, qsdist, T);
+            trav_init_q(S, P.use_bvh != 0, q.o, q.d, q.t, L.shadow, qsdist, T);
             tracing = true;
         }
         if (P.wave_trace && !t_exh && __any(L.job == -2)) t_exh = wall_clock64();

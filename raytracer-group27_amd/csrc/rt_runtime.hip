@@ -128,7 +128,6 @@ struct rt_ctx {
     int opt_fan_cap = 0;      // pixels a wave may have waiting on fans before it stops taking new ones (0: default)
     int opt_dual = -1;        // dynamic-fetch steps: record and node visit in one iteration (-1 default, 0 off, 1 on)
     int opt_variant = -1;   // -1: the shipped variant for the render shape (RT_DF_BATCH / _FRAME, RT_WT_DEFAULT)
-    int opt_ahead = -1;     // opaque-scene kernel: mirror-ahead helpers (-1 default on, 0 off)
     int opt_opaque = -1;    // opaque-scene kernel: -1 where eligible, 0 never (general kernels), 2 its 3-wave A/B build
     char last_kernel[64] = {0};
     // view batches: the camera table's pinned host staging and the event of its last copy (the buffer
@@ -827,10 +826,6 @@ static int set_option_one(rt_ctx* c, int option, int value) {
             if (value < -1 || value > 2) break;
             c->opt_opaque = value;
             return RT_OK;
-        case RT_OPT_AHEAD:
-            if (value < -1 || value > 1) break;
-            c->opt_ahead = value;
-            return RT_OK;
         default:
             set_error("rt_ctx_set_option: unknown option");
             return RT_ERR_INVALID;
@@ -1141,7 +1136,6 @@ static void shape_options(const rt_ctx* c, KParams& K) {
     // (C3 16-view batch 0.81 -> 0.71 ms/frame, C4 single frame 13.1 -> 11.1 ms; a second record per
     // step for lanes without a node visit measured slower: 0.72 / 11.4)
     K.dual = c->opt_dual >= 0 ? c->opt_dual : 1;
-    K.ahead = c->opt_ahead != 0 ? 1 : 0;
 }
 
 static int launch_render(rt_ctx* c, KParams& K, hipStream_t st, int count_mode, rt_stats* stats) {

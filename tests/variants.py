@@ -6,7 +6,7 @@ import contextlib
 
 def defaults(R):
     return {R.OPT_KERNEL: R.KERNEL_AUTO, R.OPT_VARIANT: -1, R.OPT_COOP: -1, R.OPT_COOP_MAX: 0, R.OPT_REFILL: 0,
-            R.OPT_FAN: 1, R.OPT_INTERLEAVE: -1, R.OPT_FAN_CAP: 0, R.OPT_DUAL_STEP: -1, R.OPT_OPAQUE: -1, R.OPT_AHEAD: -1}
+            R.OPT_FAN: 1, R.OPT_INTERLEAVE: -1, R.OPT_FAN_CAP: 0, R.OPT_DUAL_STEP: -1, R.OPT_OPAQUE: -1}
 
 
 def kernel_classes(R):
@@ -34,8 +34,7 @@ def all_variants(R):
         {R.OPT_KERNEL: df, R.OPT_OPAQUE: 0},                    # general kernels where the opaque one is eligible
         {R.OPT_KERNEL: df, R.OPT_OPAQUE: 2},                    # the opaque kernel's 3-wave build
         {R.OPT_KERNEL: df, R.OPT_REFILL: 32},                   # ... and a half-wave refill
-        {R.OPT_KERNEL: df, R.OPT_AHEAD: 0},                     # ... without mirror-ahead helpers
-        {R.OPT_KERNEL: df, R.OPT_COOP: 0},                      # ... helpers without the drain lane groups
+        {R.OPT_KERNEL: df, R.OPT_COOP: 1},                      # ... drain lane groups in the drain only
     ]
     return out
 

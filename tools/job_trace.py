@@ -1,6 +1,6 @@
 """Developer tool: per-job (pixel) latency of one frame from the persistent kernel's job trace
 (RT_OPT_WAVE_TRACE): start / end times, queries per job, the slowest jobs and when jobs started.
-Usage: python tools/job_trace.py C4 [fan=0|1] [opaque=0|-1] [ahead=0|-1] [coop=N] [refill=N] [variant=V]"""
+Usage: python tools/job_trace.py C4 [fan=0|1] [opaque=0|-1] [coop=N] [refill=N] [variant=V]"""
 import ctypes as C
 import os
 import sys
@@ -17,7 +17,7 @@ ctx = R.Context(s)
 for a in sys.argv[2:]:
     k, v = a.split("=")
     ctx.set_option({"fan": R.OPT_FAN, "variant": R.OPT_VARIANT, "refill": R.OPT_REFILL, "opaque": R.OPT_OPAQUE,
-                    "ahead": R.OPT_AHEAD, "coop": R.OPT_COOP}[k], int(v))
+                    "coop": R.OPT_COOP}[k], int(v))
 ctx.set_option(R.OPT_WAVE_TRACE, 1)
 cam = R.camera_from_trackball(aspect=R.aspect_of(W, H))
 ctx.render(cam, p, W, H)
