@@ -38,8 +38,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level para
 BAND_ROWS = 8
 DEFAULT_VIEWS = 64  # frames per step: a 64-view turntable (5.625 deg apart) of the C3 scene in one launch
 # frames per step of the other configs (a step of a few hundred ms at most): C4's 64-sample soft shadows
-# take ~10 ms per frame, C5's 4K frames with 3 x 64 plane-light samples ~0.2 s
-CONFIG_VIEWS = {"C1": 64, "C2": 64, "C3": DEFAULT_VIEWS, "C4": 16, "C5": 2}
+# take ~10 ms per frame; a C5 4K frame (3 x 64 plane-light samples, glass to depth 8: ~1e9 rays) fills the GPU
+# on its own, and batching its views measured slower per ray (2 900 vs 2 556 Mrays/s for 8 views, r02)
+CONFIG_VIEWS = {"C1": 64, "C2": 64, "C3": DEFAULT_VIEWS, "C4": 16, "C5": 1}
 
 
 def algorithmic_bytes(st, pixels):

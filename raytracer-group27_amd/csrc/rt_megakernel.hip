@@ -1090,6 +1090,21 @@ struct Trav {
 
 __device__ __forceinline__ bool leaf_pending(const Trav& T) { return T.rk > 0 || T.lh != 0u; }
 
+// a traversal state with nothing to walk (a lane without a query this phase)
+__device__ __forceinline__ void trav_idle(Trav& T) {
+    T.o = T.d = T.nd = T.inv = v3{0.0f, 0.0f, 0.0f};
+    T.thr = T.tcull = 0.0f;
+    T.best.t = 0.0f;
+    T.best.key = -1;
+    T.best.rec = RT_NO_HIT;
+    T.mask = RefMask{0u, 0u};
+    T.cur = RT_TRAV_NONE;
+    T.sp = 0;
+    T.rr = T.rk = 0;
+    T.lb = T.lc = T.lh = 0u;
+    T.found = T.ref = T.any = false;
+}
+
 // Query setup: the prologue of trace_query8 (same thresholds and flags).
 __device__ __forceinline__ void trav_init_q(const DevScene& S, bool use_bvh, v3 qo, v3 qd, float qt, bool shadow,
                                             float sdist, Trav& T) {
@@ -2127,7 +2142,6 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
     Cnt cnt{};
     int xr = (int)(blockIdx.x & 7), xtried = 0;
     bool tracing = false, pending = false;
-    const int refill_at = P.refill;
     unsigned long long t_exh = 0ull;
     for (;;) {
         // ---- phase A: advance the pending lanes, then refill the idle ones ----
@@ -2189,10 +2203,18 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
             __syncthreads();
         }
         if (COUNT) cnt.cyc_d += (unsigned long long)clock64() - tJ;
-        if (start) {
-            cnt.rays++;
-            trav_init_q(S, P.use_bvh != 0, q.o, q.d, q.t, L.shadow, qsdist, T);
-            tracing = true;
+        // full-wave phases: no lane traces across phase A, so the traversal state is rebuilt for every lane
+        // here (a new query, or an empty walk) and nothing of it has to be kept across the state machine
+        {
+            Trav Tn;
+            if (start) {
+                cnt.rays++;
+                trav_init_q(S, P.use_bvh != 0, q.o, q.d, q.t, L.shadow, qsdist, Tn);
+                tracing = true;
+            } else {
+                trav_idle(Tn);
+            }
+            T = Tn;
         }
         if (P.wave_trace && !t_exh && __any(L.job == -2)) t_exh = wall_clock64();
         if (!__any(tracing)) {
@@ -2223,11 +2245,12 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
                 tracing = false;
                 pending = true;
             }
+            // full-wave phases (refill 64, the batch and few-sample policy of the general kernel): the phase
+            // ends when no lane traces
             if (!__any(tracing)) break;
-            if (__popcll(__ballot(pending || L.job == -1)) >= refill_at) break;
             // drain (no lane can take a new job): the wave's last queries walked by lane groups, as in
             // persistent_df_kernel (coop 2: also the last ones a full-wave refill waits for)
-            if (COOP && P.coop && ((P.coop == 2 && refill_at == 64) || (!__any(L.job == -1) && __any(L.job == -2)))) {
+            if (COOP && P.coop && (P.coop == 2 || (!__any(L.job == -1) && __any(L.job == -2)))) {
                 const unsigned long long om = __ballot(tracing);
                 const int k = __popcll(om);
                 if (k <= P.coop_max) {

@@ -128,7 +128,7 @@ struct rt_ctx {
     int opt_fan_cap = 0;      // pixels a wave may have waiting on fans before it stops taking new ones (0: default)
     int opt_dual = -1;        // dynamic-fetch steps: record and node visit in one iteration (-1 default, 0 off, 1 on)
     int opt_variant = -1;   // -1: the shipped variant for the render shape (RT_DF_BATCH / _FRAME, RT_WT_DEFAULT)
-    int opt_opaque = -1;    // opaque-scene kernel: -1 where eligible, 0 never (general kernels), 2 its 3-wave A/B build
+    int opt_opaque = -1;    // opaque-scene kernel: -1 where eligible (build by render shape), 0 never, 1 / 2 the 4- / 3-wave build
     char last_kernel[64] = {0};
     // view batches: the camera table's pinned host staging and the event of its last copy (the buffer
     // is refilled only once that copy has read it)
@@ -878,8 +878,10 @@ static bool use_df(const rt_ctx* c, const KParams& K) {
 // the one A/B alternate: the batch variant with the drain lane groups, called out of line
 #define RT_DF_ALT (RT_V_CALL | RT_V_NOPF | RT_V_W4)
 // the opaque-scene kernel (rt_megakernel.hip persistent_opaque_kernel): 4 waves per SIMD
+// by render shape: view batches at 4 waves per SIMD (C3 64 views 0.558 vs 0.573 ms/frame at 3), single frames at
+// 3 (their tail is a few waves' serial chains, which run faster with more registers: 1.40-1.45 vs 1.56-1.63 ms)
 #define RT_OPAQUE_V (RT_V_W4 | RT_V_NOPF)
-#define RT_OPAQUE_V2 (RT_V_W3 | RT_V_NOPF)  // 3 waves per SIMD (A/B)
+#define RT_OPAQUE_V3 (RT_V_W3 | RT_V_NOPF)
 
 // Renders that the opaque-scene kernel draws: pixels (not rt_shade's explicit rays) of a large scene
 // (the dynamic-fetch class) whose materials are all opaque, lit by point and spot lights only, without
@@ -889,6 +891,10 @@ static bool use_df(const rt_ctx* c, const KParams& K);
 static bool opaque_path(const rt_ctx* c, const KParams& K, bool pixels) {
     return pixels && c->opt_opaque != 0 && c->opt_variant < 0 && use_df(c, K) && K.S.all_opaque && K.S.nsl == 0 &&
            K.S.nplane == 0 && !K.S.tex_on && (K.glossy_n == 1 || !c->glossy_material);
+}
+// the opaque kernel's 3-wave build: single frames (RT_OPT_OPAQUE 1 / 2 force the 4- / 3-wave build)
+static bool opaque_w3(const rt_ctx* c, const KParams& K) {
+    return c->opt_opaque == 2 || (c->opt_opaque != 1 && K.n_views <= 1);
 }
 
 // by render shape: view batches and sample-fan renders run the lean 4-wave variant (C4 single frame
@@ -921,12 +927,11 @@ static bool launch_shipped(bool df, int v, int grid, hipStream_t st, const KPara
 template <bool COUNT>
 static int launch_persistent(int grid, hipStream_t st, const KParams& K, const JobSrc& J, rt_ctx* c) {
     if (opaque_path(c, K, J.mode == 0)) {
-        if (c->opt_opaque == 2)
-            hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V2>), dim3(grid), dim3(64), 0, st, K, J);
-        else
-            hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V>), dim3(grid), dim3(64), 0, st, K, J);
+        const bool w3 = opaque_w3(c, K);
+        if (w3) hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V3>), dim3(grid), dim3(64), 0, st, K, J);
+        else hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V>), dim3(grid), dim3(64), 0, st, K, J);
         std::snprintf(c->last_kernel, sizeof(c->last_kernel), "rt::persistent_opaque_kernel<%s, %d>",
-                      COUNT ? "true" : "false", c->opt_opaque == 2 ? RT_OPAQUE_V2 : RT_OPAQUE_V);
+                      COUNT ? "true" : "false", w3 ? RT_OPAQUE_V3 : RT_OPAQUE_V);
         return RT_OK;
     }
     const bool df = use_df(c, K);
@@ -960,12 +965,12 @@ static int occupancy_of(int* per_cu) {
 // resident 64-lane blocks of the kernel (the persistent grid)
 static int persistent_grid(rt_ctx* c, const KParams& K, bool pixels) {
     if (opaque_path(c, K, pixels)) {
-        const int key = c->opt_opaque == 2 ? 1 : 0;
+        const int key = opaque_w3(c, K) ? 1 : 0;
         if (c->opaque_blocks[key] > 0) return c->opaque_blocks[key];
         int cus = 0, per_cu = 0;
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
         const hipError_t e =
-            key ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V2>, 64, 0)
+            key ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V3>, 64, 0)
                 : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V>, 64, 0);
         if (e != hipSuccess || per_cu <= 0) per_cu = 8;
         c->opaque_blocks[key] = std::max(1, cus) * per_cu;
