@@ -435,92 +435,102 @@ public:
     rt_ctx* handle() const { return ctx_; }
 
     // Push the scene's current lights and materials to the device when they changed (the reference
-    // reads scene.pointLights & co. and scene.meshes[i].material on every getFinalColor call).
+    // reads scene.pointLights & co. and scene.meshes[i].material on every getFinalColor call).  The
+    // comparison walks the scene in place against the last pushed copy -- no allocation, no device call
+    // when nothing changed; per-ray loops that edit nothing between frames can sync once per frame and
+    // turn the per-call check off with autoSync(false).
     void sync(const Scene& sc) const {
-        rt_scene_desc d{};
-        std::vector<rt_point_light> pl;
-        std::vector<rt_spherical_light> sl;
-        std::vector<rt_spot_light> sp;
-        std::vector<rt_plane_light> pn;
-        lights_of(sc, d, &pl, &sl, &sp, &pn);
-        if (!same_lights(pl, sl, sp, pn)) {
-            check(rt_update_lights(ctx_, &d), "rt_update_lights");
-            l_pl_ = pl;
-            l_sl_ = sl;
-            l_sp_ = sp;
-            l_pn_ = pn;
-        }
         if (sc.meshes.size() != synced_mats_.size() || sc.spheres.size() != synced_sph_.size())
             throw std::runtime_error("BoundingVolumeHierarchy: the scene's geometry changed; build a new one");
-        std::vector<rt_material> mats, sm;
-        for (size_t i = 0; i < sc.meshes.size(); ++i) mats.push_back(detail::c_material(sc.meshes[i].material, mesh_tex_[i]));
-        for (const Sphere& s : sc.spheres) sm.push_back(detail::c_material(s.material, -1));
-        if (std::memcmp(mats.data(), synced_mats_.data(), mats.size() * sizeof(rt_material)) != 0 ||
-            std::memcmp(sm.data(), synced_sph_.data(), sm.size() * sizeof(rt_material)) != 0) {
-            check(rt_update_materials(ctx_, (int)mats.size(), mats.data(), (int)sm.size(), sm.data()),
+        if (lights_changed(sc)) {
+            rt_scene_desc d{};
+            lights_of(sc, d);
+            check(rt_update_lights(ctx_, &d), "rt_update_lights");
+        }
+        if (materials_changed(sc)) {
+            for (size_t i = 0; i < sc.meshes.size(); ++i) synced_mats_[i] = detail::c_material(sc.meshes[i].material, mesh_tex_[i]);
+            for (size_t i = 0; i < sc.spheres.size(); ++i) synced_sph_[i] = detail::c_material(sc.spheres[i].material, -1);
+            check(rt_update_materials(ctx_, (int)synced_mats_.size(), synced_mats_.data(), (int)synced_sph_.size(),
+                                      synced_sph_.data()),
                   "rt_update_materials");
-            synced_mats_ = mats;
-            synced_sph_ = sm;
         }
     }
+    // getFinalColor's per-call sync (default on, the reference's semantics); off: the caller syncs
+    void autoSync(bool on) { auto_sync_ = on; }
+    bool autoSync() const { return auto_sync_; }
 
 private:
-    void lights_of(const Scene& sc, rt_scene_desc& d, std::vector<rt_point_light>* pl = nullptr,
-                   std::vector<rt_spherical_light>* sl = nullptr, std::vector<rt_spot_light>* sp = nullptr,
-                   std::vector<rt_plane_light>* pn = nullptr) const {
-        std::vector<rt_point_light>& a = pl ? *pl : l_pl_;
-        std::vector<rt_spherical_light>& b = sl ? *sl : l_sl_;
-        std::vector<rt_spot_light>& c = sp ? *sp : l_sp_;
-        std::vector<rt_plane_light>& e = pn ? *pn : l_pn_;
-        a.clear();
-        b.clear();
-        c.clear();
-        e.clear();
-        for (const PointLight& l : sc.pointLights) {
-            rt_point_light x{};
-            detail::put(x.position, l.position);
-            detail::put(x.color, l.color);
-            a.push_back(x);
-        }
-        for (const SphericalLight& l : sc.sphericalLight) {
-            rt_spherical_light x{};
-            detail::put(x.position, l.position);
-            x.radius = l.radius;
-            detail::put(x.color, l.color);
-            b.push_back(x);
-        }
-        for (const SpotLight& l : sc.spotLight) {
-            rt_spot_light x{};
-            detail::put(x.position, l.position);
-            detail::put(x.direction, l.direction);
-            x.angle = l.angle;
-            detail::put(x.color, l.color);
-            c.push_back(x);
-        }
-        for (const PlaneLight& l : sc.planeLight) {
-            rt_plane_light x{};
-            detail::put(x.position, l.position);
-            detail::put(x.width, l.width);
-            detail::put(x.height, l.height);
-            detail::put(x.color, l.color);
-            e.push_back(x);
-        }
-        d.num_point_lights = (int)a.size();
-        d.point_lights = a.data();
-        d.num_spherical_lights = (int)b.size();
-        d.spherical_lights = b.data();
-        d.num_spot_lights = (int)c.size();
-        d.spot_lights = c.data();
-        d.num_plane_lights = (int)e.size();
-        d.plane_lights = e.data();
+    static rt_point_light conv(const PointLight& l) {
+        rt_point_light x{};
+        detail::put(x.position, l.position);
+        detail::put(x.color, l.color);
+        return x;
     }
-    template <class T>
-    static bool same(const std::vector<T>& x, const std::vector<T>& y) {
-        return x.size() == y.size() && std::memcmp(x.data(), y.data(), x.size() * sizeof(T)) == 0;
+    static rt_spherical_light conv(const SphericalLight& l) {
+        rt_spherical_light x{};
+        detail::put(x.position, l.position);
+        x.radius = l.radius;
+        detail::put(x.color, l.color);
+        return x;
     }
-    bool same_lights(const std::vector<rt_point_light>& a, const std::vector<rt_spherical_light>& b,
-                     const std::vector<rt_spot_light>& c, const std::vector<rt_plane_light>& e) const {
-        return same(a, l_pl_) && same(b, l_sl_) && same(c, l_sp_) && same(e, l_pn_);
+    static rt_spot_light conv(const SpotLight& l) {
+        rt_spot_light x{};
+        detail::put(x.position, l.position);
+        detail::put(x.direction, l.direction);
+        x.angle = l.angle;
+        detail::put(x.color, l.color);
+        return x;
+    }
+    static rt_plane_light conv(const PlaneLight& l) {
+        rt_plane_light x{};
+        detail::put(x.position, l.position);
+        detail::put(x.width, l.width);
+        detail::put(x.height, l.height);
+        detail::put(x.color, l.color);
+        return x;
+    }
+    template <class L, class T>
+    static bool differs(const std::vector<L>& src, const std::vector<T>& pushed) {
+        if (src.size() != pushed.size()) return true;
+        for (size_t i = 0; i < src.size(); ++i) {
+            const T x = conv(src[i]);
+            if (std::memcmp(&x, &pushed[i], sizeof(T)) != 0) return true;
+        }
+        return false;
+    }
+    bool lights_changed(const Scene& sc) const {
+        return differs(sc.pointLights, l_pl_) || differs(sc.sphericalLight, l_sl_) || differs(sc.spotLight, l_sp_) ||
+               differs(sc.planeLight, l_pn_);
+    }
+    bool materials_changed(const Scene& sc) const {
+        for (size_t i = 0; i < sc.meshes.size(); ++i) {
+            const rt_material m = detail::c_material(sc.meshes[i].material, mesh_tex_[i]);
+            if (std::memcmp(&m, &synced_mats_[i], sizeof m) != 0) return true;
+        }
+        for (size_t i = 0; i < sc.spheres.size(); ++i) {
+            const rt_material m = detail::c_material(sc.spheres[i].material, -1);
+            if (std::memcmp(&m, &synced_sph_[i], sizeof m) != 0) return true;
+        }
+        return false;
+    }
+    // the scene's lights into the pushed copies l_*_ and d's pointers to them
+    void lights_of(const Scene& sc, rt_scene_desc& d) const {
+        l_pl_.clear();
+        l_sl_.clear();
+        l_sp_.clear();
+        l_pn_.clear();
+        for (const PointLight& l : sc.pointLights) l_pl_.push_back(conv(l));
+        for (const SphericalLight& l : sc.sphericalLight) l_sl_.push_back(conv(l));
+        for (const SpotLight& l : sc.spotLight) l_sp_.push_back(conv(l));
+        for (const PlaneLight& l : sc.planeLight) l_pn_.push_back(conv(l));
+        d.num_point_lights = (int)l_pl_.size();
+        d.point_lights = l_pl_.data();
+        d.num_spherical_lights = (int)l_sl_.size();
+        d.spherical_lights = l_sl_.data();
+        d.num_spot_lights = (int)l_sp_.size();
+        d.spot_lights = l_sp_.data();
+        d.num_plane_lights = (int)l_pn_.size();
+        d.plane_lights = l_pn_.data();
     }
 
     Scene* scene_ = nullptr;
@@ -531,6 +541,7 @@ private:
     mutable std::vector<rt_spherical_light> l_sl_;
     mutable std::vector<rt_spot_light> l_sp_;
     mutable std::vector<rt_plane_light> l_pn_;
+    bool auto_sync_ = true;
 };
 
 // ---- camera (framework/src/trackball.cpp:15-98; mouse handling out of scope) ----
@@ -627,7 +638,7 @@ private:
 // getFinalColor(scene, bvh, ray, level) (src/main.cpp:129): one ray through rt_shade; `level` starts
 // the recursion at that depth (the reference's `level >= max_reflection_level` stop).
 inline vec3 getFinalColor(Scene& scene, const BoundingVolumeHierarchy& bvh, Ray ray, int level = 0) {
-    bvh.sync(scene);
+    if (bvh.autoSync()) bvh.sync(scene);
     rt_ray r{{ray.origin.x, ray.origin.y, ray.origin.z}, {ray.direction.x, ray.direction.y, ray.direction.z}, ray.t};
     const rt_params p = current_params(level);
     float rgb[3] = {0, 0, 0};

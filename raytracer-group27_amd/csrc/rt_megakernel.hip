@@ -1698,7 +1698,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
     for (;;) {
         // ---- phase A: advance the pending lanes, then refill the idle ones ----
         unsigned long long tA = COUNT ? (unsigned long long)clock64() : 0ull;
-        if (P.wave_trace && t_exh) pa_drain++;
+        if (COUNT && P.wave_trace && t_exh) pa_drain++;
         bool start = false;
         Query q;
         bool qshadow = false;  // the new query's kind and cansee distance
@@ -1918,7 +1918,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
             if (!__any(tracing)) break;
             if (__popcll(__ballot(pending || L.job == -1 || (!tracing && (fans || own_fan >= 0 || fan_req)))) >= refill_at)
                 break;
-            if (P.wave_trace && t_exh) {
+            if (COUNT && P.wave_trace && t_exh) {
                 it_drain++;
                 lanes_drain += (unsigned int)__popcll(__ballot(tracing));
             }
@@ -1949,7 +1949,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
                         cnt.tris += nv.y;
                     }
                     if (tracing) coop_get(T, coop_q, r);
-                    if (P.wave_trace) coop_n++;
+                    if (COUNT && P.wave_trace) coop_n++;
                 }
             }
         }
@@ -2143,9 +2143,11 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
     int xr = (int)(blockIdx.x & 7), xtried = 0;
     bool tracing = false, pending = false;
     unsigned long long t_exh = 0ull;
+    unsigned int it_drain = 0, lanes_drain = 0, coop_n = 0, pa_drain = 0;  // wave trace, counting builds only
     for (;;) {
         // ---- phase A: advance the pending lanes, then refill the idle ones ----
         unsigned long long tA = COUNT ? (unsigned long long)clock64() : 0ull;
+        if (COUNT && P.wave_trace && t_exh) pa_drain++;
         bool start = false;
         Query q;
         float qsdist = 0.0f;
@@ -2248,6 +2250,10 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
             // full-wave phases (refill 64, the batch and few-sample policy of the general kernel): the phase
             // ends when no lane traces
             if (!__any(tracing)) break;
+            if (COUNT && P.wave_trace && t_exh) {
+                it_drain++;
+                lanes_drain += (unsigned int)__popcll(__ballot(tracing));
+            }
             // drain (no lane can take a new job): the wave's last queries walked by lane groups, as in
             // persistent_df_kernel (coop 2: also the last ones a full-wave refill waits for)
             if (COOP && P.coop && (P.coop == 2 || (!__any(L.job == -1) && __any(L.job == -2)))) {
@@ -2272,6 +2278,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
                         cnt.tris += nv.y;
                     }
                     if (tracing) coop_get(T, coop_q, r);
+                    if (COUNT && P.wave_trace) coop_n++;
                 }
             }
         }
@@ -2284,7 +2291,10 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
         w[1] = wall_clock64();
         w[2] = wave_jobs;
         w[3] = t_exh;
-        for (int k = 4; k < 8; ++k) w[k] = 0ull;
+        w[4] = it_drain;
+        w[5] = lanes_drain;
+        w[6] = coop_n;
+        w[7] = pa_drain;
     }
 }
 

@@ -96,6 +96,24 @@ int main(int argc, char** argv) {
         }
         std::printf("views_identical=%d/%d\n", same, (int)cams.size());
 
+        // 5b. autoSync(false): a per-ray loop that syncs the scene itself, once
+        {
+            const Ray ray = camera.generateRay(vec2{0.05f, 0.05f});
+            const vec3 before = getFinalColor(scene, bvh, ray);
+            const vec3 kd = scene.meshes[0].material.kd;
+            bvh.autoSync(false);
+            scene.meshes[0].material.kd = vec3(0.9f, 0.1f, 0.1f);
+            const vec3 stale = getFinalColor(scene, bvh, ray);
+            bvh.sync(scene);
+            const vec3 fresh = getFinalColor(scene, bvh, ray);
+            bvh.autoSync(true);
+            scene.meshes[0].material.kd = kd;
+            const vec3 back = getFinalColor(scene, bvh, ray);
+            auto eq = [](const vec3& a, const vec3& b) { return a.x == b.x && a.y == b.y && a.z == b.z; };
+            std::printf("autosync stale_same=%d fresh_differs=%d restored=%d\n", eq(before, stale) ? 1 : 0,
+                        eq(before, fresh) ? 0 : 1, eq(before, back) ? 1 : 0);
+        }
+
         // 6. Screen + bloom + gamma + BMP, as the "Render to file" button does
         Screen scr{32, 24};
         scr.setBloomFilter(FilteringOption::BloomWithReinhardHdr);

@@ -40,6 +40,7 @@ def test_facade_matches_oracle_on_gpu(R, O, tmp_path):
     r = subprocess.run([exe, R.data_dir(), str(tmp_path)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "views_identical=3/3" in r.stdout, r.stdout
+    assert "autosync stale_same=1 fresh_differs=1 restored=1" in r.stdout, r.stdout
 
     def load(name, cols):
         return np.fromfile(str(tmp_path / f"{name}.bin"), np.float32).reshape(-1, cols)

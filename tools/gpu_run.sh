@@ -12,7 +12,7 @@
 #   pmc[:CFG[:VIEWS]]           the PMC counter groups of tools/pmc_counters.txt (tools/profile.sh)
 #   ab:CFGS:VIEWS:ROUNDS[:ARMS] tools/ab_variants.py (CFGS / ARMS comma-separated; ARMS name=k=v;k=v)
 #   simd[:CFG[:VIEWS]]          tools/simd_eff.py (counting build: lanes per node / record step)
-#   wave[:CFG[:VIEWS]]          tools/wave_trace.py (per-wave start / drain / end)
+#   wave[:CFG[:VIEWS[:COUNT]]]  tools/wave_trace.py (per-wave start / drain / end; COUNT 1: counting build)
 #   jobs[:CFG[:OPTS]]           tools/job_trace.py (per-pixel query chains of a single frame; OPTS k=v;k=v)
 #   ranks                       bench.py N = 2 on this one GPU (gloo control plane, IPC exchange)
 #   cpu_baseline                tools/cpu_baseline.py (BASELINE.md's full CPU samples on the host)
@@ -45,7 +45,7 @@ for step in "$@"; do
     ab)    ARMS=(); if [ -n "$d" ]; then for x in ${d//,/ }; do ARMS+=("${x//;/,}"); done; ARMS=(--arms "${ARMS[@]/=/:}"); fi
            run 900 ab_${TAG}.log python -u tools/ab_variants.py ${a//,/ } --views ${b:-16} --rounds ${c:-3} "${ARMS[@]}" ;;
     simd)  run 300 simd_${TAG}.log env SE_VIEWS=${b:-16} python tools/simd_eff.py ${a:-C3} ;;
-    wave)  run 300 wave_${TAG}.log env WT_VIEWS=${b:-1} python tools/wave_trace.py ${a:-C3} ;;
+    wave)  run 300 wave_${TAG}${c:+_count}.log env WT_VIEWS=${b:-1} WT_COUNT=${c:-0} python tools/wave_trace.py ${a:-C3} ;;
     jobs)  run 300 jobs_${TAG}${b:+_$b}.log python tools/job_trace.py ${a:-C3} ${b//;/ } ;;
     ranks) run 600 ranks_${TAG}.json env BENCH_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29555 bench.py --gpus 2 --steps 5 --warmup 1 --no-single-frame ;;
     cpu_baseline) run 1500 cpu_baseline_${TAG}.json python tools/cpu_baseline.py --out gpurun_out/cpu_baseline_${TAG}.out.json ;;

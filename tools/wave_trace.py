@@ -1,7 +1,9 @@
 """Developer tool: per-wave timeline of the persistent render kernel (context option RT_OPT_WAVE_TRACE) -- launch
 skew, when each wave found the job queue empty, and what it did until it retired (drain
 iterations, tracing lanes per iteration, state-machine passes).
-Usage: python tools/wave_trace.py C3 [C4 ...]"""
+Usage: python tools/wave_trace.py C3 [C4 ...]
+The opaque-scene kernel fills the drain columns (iterations, lanes, lane-group walks, phase-A passes) in its
+counting build only (WT_COUNT=1 -- the shipped build keeps those counters out of its registers)."""
 import ctypes as C
 import os
 import sys
@@ -23,6 +25,8 @@ for cfg in [a for a in sys.argv[1:] if a.startswith("C")] or ["C3"]:
     s, p, W, H, desc = R.build_config(cfg)
     ctx = R.Context(s)
     ctx.set_option(R.OPT_WAVE_TRACE, 1)
+    if os.environ.get("WT_COUNT") == "1":
+        R.lib().rt_set_counting(1)
     cam = R.camera_from_trackball(aspect=R.aspect_of(W, H))
     V = int(os.environ.get("WT_VIEWS", "1"))  # > 1: a V-view turntable batch in one launch
     if V > 1:
@@ -55,6 +59,7 @@ for cfg in [a for a in sys.argv[1:] if a.startswith("C")] or ["C3"]:
         print("  lanes/iter pct   " + pct(t[dr, 5] / it))
         print("  us/iter pct      " + pct(drain / it))
         print("  drain phase-A passes pct " + pct(t[dr, 7]))
+        print("  lane-group walks pct " + pct(t[dr, 6]))
         last = np.argsort(end)[-5:]
         for i in last:
             print(f"   last wave {i}: end {end[i]:.1f} dry {(t[i, 3] - t0) / 100.0:.1f} iters {t[i, 4]} "
