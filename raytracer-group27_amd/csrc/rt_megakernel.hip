@@ -47,6 +47,17 @@ __device__ __forceinline__ const KParams& kernel_params(const void* ka) {
     return *(const KParams*)uniform_kernarg(ka);
 }
 
+// The kernarg segment pointer made opaque to the optimiser: reads through it are scalar loads issued
+// where they are used (the scalar cache serves them), instead of kernel arguments the compiler loads
+// once and keeps in SGPRs across the whole persistent loop -- ~100 dwords of KParams that otherwise
+// spill into VGPR lanes and cost a v_readlane per use.
+__device__ __forceinline__ const char* fresh_kernarg(const void* ka) {
+    uint32_t lo = (uint32_t)(uint64_t)ka, hi = (uint32_t)((uint64_t)ka >> 32);
+    asm volatile("" : "+s"(lo), "+s"(hi));
+    typedef const __attribute__((address_space(4))) char* CB;
+    return (const char*)(CB)(((uint64_t)hi << 32) | lo);
+}
+
 // Per-lane state between queries: the pixel, the position in the recursion tree and in the light
 // loop of the current shading point.  Kept small (39 dwords without textures): it is live across
 // every traversal step.
@@ -2124,17 +2135,19 @@ __device__ __forceinline__ bool lite_advance(const KParams& P, LiteLane& L, bool
 }
 
 template <bool COUNT, int V>
-__global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KParams P, JobSrc J) {
+__global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KParams, JobSrc) {
     constexpr bool PF = !(V & RT_V_NOPF), COOP = !(V & RT_V_NOCOOP);
+    // the kernel's arguments are read where each phase uses them (fresh_kernarg), not held in SGPRs
+    const void* ka = (const void*)__builtin_amdgcn_kernarg_segment_ptr();
+#define RT_FRESH const KParams& P = *(const KParams*)fresh_kernarg(ka); const DevScene& S = P.S
     __shared__ int stack_lds[RT_STACK8 * RT_WAVE];
     __shared__ int coop_pool[COOP_POOL];   // drain lane groups (COOP): node groups of the wave's last queries
     __shared__ int coop_q[CQ_N * COOP_Q];  // ... and those queries
     __shared__ int s_base, s_lim;
     const int lane_id = threadIdx.x;
     int* stk = stack_lds + lane_id;
-    const unsigned long long t_wave0 = P.wave_trace ? wall_clock64() : 0ull;
+    const unsigned long long t_wave0 = kernel_params(ka).wave_trace ? wall_clock64() : 0ull;
     unsigned int wave_jobs = 0;
-    const DevScene& S = P.S;
     LiteLane L;
     L.job = -1;
     L.shadow = false;
@@ -2147,6 +2160,8 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
     for (;;) {
         // ---- phase A: advance the pending lanes, then refill the idle ones ----
         unsigned long long tA = COUNT ? (unsigned long long)clock64() : 0ull;
+        RT_FRESH;
+        const JobSrc& J = kernel_jobs(&P);
         if (COUNT && P.wave_trace && t_exh) pa_drain++;
         bool start = false;
         Query q;
@@ -2255,35 +2270,43 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
                 lanes_drain += (unsigned int)__popcll(__ballot(tracing));
             }
             // drain (no lane can take a new job): the wave's last queries walked by lane groups, as in
-            // persistent_df_kernel (coop 2: also the last ones a full-wave refill waits for)
-            if (COOP && P.coop && (P.coop == 2 || (!__any(L.job == -1) && __any(L.job == -2)))) {
-                const unsigned long long om = __ballot(tracing);
-                const int k = __popcll(om);
-                if (k <= P.coop_max) {
-                    int G = 64;
-                    while (G > 1 && k * G > 64) G >>= 1;
-                    const int r = __popcll(om & ((1ull << lane_id) - 1ull));
-                    if (tracing) {
-                        coop_put(T, coop_q, r);
-                        int* gp = coop_pool + r * (COOP_POOL * G / 64);
-                        for (int j = 0; j < T.sp; ++j) gp[j] = stk[j * RT_WAVE];
-                        if (T.cur != RT_TRAV_NONE) gp[T.sp] = (int)T.cur;
-                    }
-                    __syncthreads();
-                    const uint2 nv = coop_group_trace<8>(S.nodes, S.tri, S.refn, S.leaf_path, coop_pool, coop_q, om,
-                                                         P.coop_reserve);
-                    __syncthreads();
-                    if (COUNT) {
-                        cnt.nodes += nv.x;
-                        cnt.tris += nv.y;
-                    }
-                    if (tracing) coop_get(T, coop_q, r);
-                    if (COUNT && P.wave_trace) coop_n++;
-                }
+            // persistent_df_kernel (coop 2: also the last ones a full-wave refill waits for).  The lane
+            // groups run after the loop, so their registers do not add to the traversal loop's
+            if (COOP && P.coop && (P.coop == 2 || (!__any(L.job == -1) && __any(L.job == -2))) &&
+                __popcll(__ballot(tracing)) <= P.coop_max)
+                break;
+        }
+        if (COOP && __any(tracing)) {
+            const unsigned long long om = __ballot(tracing);
+            const int k = __popcll(om);
+            int G = 64;
+            while (G > 1 && k * G > 64) G >>= 1;
+            const int r = __popcll(om & ((1ull << lane_id) - 1ull));
+            if (tracing) {
+                coop_put(T, coop_q, r);
+                int* gp = coop_pool + r * (COOP_POOL * G / 64);
+                for (int j = 0; j < T.sp; ++j) gp[j] = stk[j * RT_WAVE];
+                if (T.cur != RT_TRAV_NONE) gp[T.sp] = (int)T.cur;
             }
+            __syncthreads();
+            const uint2 nv =
+                coop_group_trace<8>(S.nodes, S.tri, S.refn, S.leaf_path, coop_pool, coop_q, om, P.coop_reserve);
+            __syncthreads();
+            if (COUNT) {
+                cnt.nodes += nv.x;
+                cnt.tris += nv.y;
+            }
+            if (tracing) {
+                coop_get(T, coop_q, r);
+                trav_finish(S, T);
+                tracing = false;
+                pending = true;
+            }
+            if (COUNT && P.wave_trace) coop_n++;
         }
         if (COUNT) cnt.cyc_b += (unsigned long long)clock64() - tB;
     }
+    const KParams& P = kernel_params(ka);
     flush_counters<COUNT>(P, cnt);
     if (P.wave_trace && lane_id == 0) {
         unsigned long long* w = P.wave_trace + 8 * blockIdx.x;
@@ -2296,6 +2319,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
         w[6] = coop_n;
         w[7] = pa_drain;
     }
+#undef RT_FRESH
 }
 
 // BoundingVolumeHierarchy::intersect(ray, hitInfo, useBVH) per ray (rt_intersect): the same
