@@ -1665,10 +1665,12 @@ __device__ __forceinline__ void fan_record(FanTable& ft, int f, int s, bool vis,
 }
 
 template <bool COUNT, bool TEX, int V>
-__global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParams P, JobSrc J) {
+__global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParams, JobSrc) {
     // drain lane groups: inline, or out of line with the out-of-line state machine (RT_V_CALL)
     constexpr bool PF = !(V & RT_V_NOPF), COOP = !(V & RT_V_NOCOOP), FANS = (V & RT_V_FAN) != 0;
-    const bool fan_on = FANS && P.fan;  // (the host sets P.fan only for FANS variants)
+    // the kernel's arguments (P, J) are read where each pass uses them (fresh_kernarg), not held in SGPRs
+    const void* ka = (const void*)__builtin_amdgcn_kernarg_segment_ptr();
+    const bool fan_on = FANS && kernel_params(ka).fan;  // (the host sets P.fan only for FANS variants)
     __shared__ int stack_lds[RT_STACK8 * RT_WAVE];
     __shared__ int coop_pool[COOP_POOL];   // drain: node groups of the wave's last queries
     __shared__ int coop_q[CQ_N * COOP_Q];  // drain: those queries
@@ -1676,10 +1678,8 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
     __shared__ FanTable ft;
     const int lane_id = threadIdx.x;
     int* stk = stack_lds + lane_id;
-    const void* ka = (const void*)__builtin_amdgcn_kernarg_segment_ptr();  // this kernel's (P, J)
-    const unsigned long long t_wave0 = P.wave_trace ? wall_clock64() : 0ull;
+    const unsigned long long t_wave0 = kernel_params(ka).wave_trace ? wall_clock64() : 0ull;
     unsigned int wave_jobs = 0;  // jobs this wave took (wave trace)
-    const DevScene& S = P.S;
     if (FANS) {
         if (lane_id < FAN_SLOTS) ft.owner[lane_id] = -1;
         __syncthreads();
@@ -1702,13 +1702,16 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
     int xr = (int)(blockIdx.x & 7), xtried = 0;  // J.xq: the job range this wave draws from, ranges used up
     bool tracing = false;                        // a query is in flight
     bool pending = false;                        // a finished query waits for advance_lane
-    const int refill_at = P.refill;
+    const int refill_at = kernel_params(ka).refill;
     // wave trace of the drain (after this wave first found the job queue empty)
     unsigned long long t_exh = 0ull;
     unsigned int it_drain = 0, lanes_drain = 0, coop_n = 0, pa_drain = 0;
     for (;;) {
         // ---- phase A: advance the pending lanes, then refill the idle ones ----
         unsigned long long tA = COUNT ? (unsigned long long)clock64() : 0ull;
+        const KParams& P = *(const KParams*)fresh_kernarg(ka);
+        const JobSrc& J = kernel_jobs(&P);
+        const DevScene& S = P.S;
         if (COUNT && P.wave_trace && t_exh) pa_drain++;
         bool start = false;
         Query q;
@@ -1907,6 +1910,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
         }
         float4 g[8];
         if (PF && tracing && T.cur != RT_TRAV_NONE) node_fetch(S.nodes, T.cur, g);
+        bool coop_now = false;
         for (;;) {
             if (COUNT) {
                 const int ntr = __popcll(__ballot(tracing));  // (wave-wide: before the leader branch)
@@ -1934,38 +1938,48 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
                 lanes_drain += (unsigned int)__popcll(__ballot(tracing));
             }
             // drain (no lane can take a new job): the remaining queries go to lane groups
-            // (coop 2: also in steady state, for the last queries a full-wave refill waits for)
-            if (COOP && P.coop && ((P.coop == 2 && refill_at == 64) || (!__any(L.job == -1) && __any(L.job == -2)))) {
-                const unsigned long long om = __ballot(tracing);
-                const int k = __popcll(om);
-                if (k <= P.coop_max) {
-                    int G = 64;
-                    while (G > 1 && k * G > 64) G >>= 1;
-                    const int r = __popcll(om & ((1ull << lane_id) - 1ull));
-                    if (tracing) {
-                        coop_put(T, coop_q, r);
-                        int* gp = coop_pool + r * (COOP_POOL * G / 64);
-                        for (int j = 0; j < T.sp; ++j) gp[j] = stk[j * RT_WAVE];
-                        if (T.cur != RT_TRAV_NONE) gp[T.sp] = (int)T.cur;
-                    }
-                    __syncthreads();
-                    const uint2 nv =
-                        (V & RT_V_CALL) ? coop_group_trace_call<8>(S.nodes, S.tri, S.refn, S.leaf_path, coop_pool,
-                                                                   coop_q, om, P.coop_reserve)
-                                        : coop_group_trace<8>(S.nodes, S.tri, S.refn, S.leaf_path, coop_pool, coop_q,
-                                                              om, P.coop_reserve);
-                    __syncthreads();
-                    if (COUNT) {
-                        cnt.nodes += nv.x;
-                        cnt.tris += nv.y;
-                    }
-                    if (tracing) coop_get(T, coop_q, r);
-                    if (COUNT && P.wave_trace) coop_n++;
-                }
+            // (coop 2: also in steady state, for the last queries a full-wave refill waits for); the
+            // lane groups run after the loop, so their registers do not add to the traversal loop's
+            if (COOP && P.coop && ((P.coop == 2 && refill_at == 64) || (!__any(L.job == -1) && __any(L.job == -2))) &&
+                __popcll(__ballot(tracing)) <= P.coop_max) {
+                coop_now = true;
+                break;
             }
+        }
+        if (COOP && coop_now) {
+            const unsigned long long om = __ballot(tracing);
+            const int k = __popcll(om);
+            int G = 64;
+            while (G > 1 && k * G > 64) G >>= 1;
+            const int r = __popcll(om & ((1ull << lane_id) - 1ull));
+            if (tracing) {
+                coop_put(T, coop_q, r);
+                int* gp = coop_pool + r * (COOP_POOL * G / 64);
+                for (int j = 0; j < T.sp; ++j) gp[j] = stk[j * RT_WAVE];
+                if (T.cur != RT_TRAV_NONE) gp[T.sp] = (int)T.cur;
+            }
+            __syncthreads();
+            const uint2 nv =
+                (V & RT_V_CALL) ? coop_group_trace_call<8>(S.nodes, S.tri, S.refn, S.leaf_path, coop_pool, coop_q, om,
+                                                           P.coop_reserve)
+                                : coop_group_trace<8>(S.nodes, S.tri, S.refn, S.leaf_path, coop_pool, coop_q, om,
+                                                      P.coop_reserve);
+            __syncthreads();
+            if (COUNT) {
+                cnt.nodes += nv.x;
+                cnt.tris += nv.y;
+            }
+            if (tracing) {
+                coop_get(T, coop_q, r);
+                trav_finish(S, T);
+                tracing = false;
+                pending = true;
+            }
+            if (COUNT && P.wave_trace) coop_n++;
         }
         if (COUNT) cnt.cyc_b += (unsigned long long)clock64() - tB;
     }
+    const KParams& P = kernel_params(ka);
     flush_counters<COUNT>(P, cnt);
     if (P.wave_trace && lane_id == 0) {  // wave trace, 100 MHz clock: start, end, jobs, drain
         unsigned long long* w = P.wave_trace + 8 * blockIdx.x;
@@ -2146,7 +2160,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
     __shared__ int s_base, s_lim;
     const int lane_id = threadIdx.x;
     int* stk = stack_lds + lane_id;
-    const unsigned long long t_wave0 = kernel_params(ka).wave_trace ? wall_clock64() : 0ull;
+    const unsigned long long t_wave0 = (COUNT && kernel_params(ka).wave_trace) ? wall_clock64() : 0ull;
     unsigned int wave_jobs = 0;
     LiteLane L;
     L.job = -1;
@@ -2173,7 +2187,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
             q.d = T.d;
             const int jb = L.job;
             start = lite_advance<COUNT>(P, L, T.found, T.best, q, qsdist, cnt);
-            if (P.job_trace && L.job == -1) P.job_trace[3 * jb + 1] = wall_clock64();
+            if (COUNT && P.job_trace && L.job == -1) P.job_trace[3 * jb + 1] = wall_clock64();
         }
         const unsigned long long tJ = COUNT ? (unsigned long long)clock64() : 0ull;
         if (COUNT) cnt.cyc_c += tJ - tA;
@@ -2197,7 +2211,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
             if (idle) {
                 const int job_k = base + __popcll(want & ((1ull << lane_id) - 1ull));
                 if (job_k < lim) {
-                    if (P.job_trace) P.job_trace[3 * job_k] = wall_clock64();
+                    if (COUNT && P.job_trace) P.job_trace[3 * job_k] = wall_clock64();
                     int out_row;
                     L.job = job_k;
                     if (job_pixel(P, job_k, L.rpix, out_row)) {
@@ -2233,7 +2247,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
             }
             T = Tn;
         }
-        if (P.wave_trace && !t_exh && __any(L.job == -2)) t_exh = wall_clock64();
+        if (COUNT && P.wave_trace && !t_exh && __any(L.job == -2)) t_exh = wall_clock64();
         if (!__any(tracing)) {
             if (!__any(L.job == -1 || pending)) break;  // every lane exhausted
             continue;
@@ -2308,7 +2322,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
     }
     const KParams& P = kernel_params(ka);
     flush_counters<COUNT>(P, cnt);
-    if (P.wave_trace && lane_id == 0) {
+    if (COUNT && P.wave_trace && lane_id == 0) {  // traces: counting build only
         unsigned long long* w = P.wave_trace + 8 * blockIdx.x;
         w[0] = t_wave0;
         w[1] = wall_clock64();

@@ -1099,14 +1099,15 @@ static int fill_params(rt_ctx* c, const rt_camera* cam, const rt_params* p, int 
     const bool few_samples = K.S.nsl * K.sl_count + K.S.nplane * K.plane_k * K.plane_k <= 4;
     K.refill = few_samples ? 64 : 24;
     K.coop = few_samples ? 2 : 1;
-    // a group of G lanes owns COOP_POOL * G / 64 pool slots: the depth-first reserve plus one breadth
-    // step must fit; coop_max = the largest query count whose groups still do
+    // a group of G lanes owns COOP_POOL * G / 64 pool slots: the depth-first reserve plus a breadth
+    // step of min(G, 4) nodes must fit (coop_group_trace narrows its steps to the free slots above the
+    // reserve); coop_max = the largest query count whose groups still do
     K.coop_reserve = 7 * (c->bvh8_depth + 1) + 8;
     K.coop_max = 0;
     for (int k = 1; k <= COOP_Q; ++k) {
         int G = 64;
         while (G > 1 && k * G > 64) G >>= 1;
-        if (COOP_POOL * G / 64 >= K.coop_reserve + 8 * G) K.coop_max = k;
+        if (COOP_POOL * G / 64 >= K.coop_reserve + 8 * std::min(G, 4)) K.coop_max = k;
     }
     return RT_OK;
 }

@@ -1,6 +1,7 @@
 """Developer tool: per-job (pixel) latency of one frame from the persistent kernel's job trace
 (RT_OPT_WAVE_TRACE): start / end times, queries per job, the slowest jobs and when jobs started.
-Usage: python tools/job_trace.py C4 [fan=0|1] [opaque=0|-1] [coop=N] [refill=N] [variant=V]"""
+Usage: python tools/job_trace.py C4 [fan=0|1] [opaque=0|-1] [coop=N] [refill=N] [variant=V]
+(the opaque-scene kernel keeps its trace stores out of the shipped build: its trace comes from the counting build)"""
 import ctypes as C
 import os
 import sys
@@ -20,7 +21,11 @@ for a in sys.argv[2:]:
                     "coop": R.OPT_COOP}[k], int(v))
 ctx.set_option(R.OPT_WAVE_TRACE, 1)
 cam = R.camera_from_trackball(aspect=R.aspect_of(W, H))
-ctx.render(cam, p, W, H)
+_, st = ctx.render(cam, p, W, H)
+if "opaque" in st.kernel_name:  # the opaque-scene kernel records its traces in the counting build only
+    R.lib().rt_set_counting(1)
+    print("(opaque-scene kernel: counting build)")
+    ctx.render(cam, p, W, H)
 _, st = ctx.render(cam, p, W, H)
 nj = 1 << 23
 buf = np.zeros(3 * nj, np.uint64)
