@@ -287,6 +287,8 @@ struct FanResult {
     uint64_t vis;
     const float* inten;  // LDS; null for opaque scenes (every intensity is 1)
     bool done;           // the lane resumes from its fan (its own last query is not a cansee segment)
+    const float* term;   // plane-light fans (LDS): each visible sample's hit term, computed by its sample lane
+    float c2max;         // ... and the running maximum of the visible samples' specular cosines
 };
 
 __device__ __forceinline__ bool start_cansee(Lane& L, v3 target, Query& q) {
@@ -491,26 +493,18 @@ __device__ __forceinline__ bool advance_lights_body(const KParams& P, Lane& L, b
                     L.ls = k * k;  // not in front of the light: no samples
                 }
             } else if (have_result && L.ls == -2) {
-                // the whole fan: the loop's accumulation replayed in sample order (px stepped by the
-                // same additions), each visible sample with its traced intensity
+                // the whole fan: the loop's accumulation replayed in sample order, each visible sample
+                // with its traced intensity and the hit term its sample lane computed with the loop's
+                // arithmetic (fan_plane_term); maxCos, a maximum, is order-free and came as one value
                 have_result = false;
-                const v3 dx = (1.0f / (float)(k - 1)) * w, dy = (1.0f / (float)(k - 1)) * h;
                 for (int s = 0; s < k * k; ++s) {
                     if ((fan.vis >> s) & 1ull) {
-                        const v3 px = L.u0;
                         L.a3 += fan.inten ? fan.inten[s] : 1.0f;
-                        const float dn = dot(normalize(L.hp - px), normal);
-                        L.a0 += ((dn < 0.0f) ? 0.0f : dn) / length(L.hp - px);
+                        L.a0 += fan.term[s];
                         L.a1 += 1.0f;
-                        const float c2 = dot(lane_nR(L), normalize(px - L.hp));
-                        L.a2 = (L.a2 < c2) ? c2 : L.a2;
-                    }
-                    L.u0 = L.u0 + dx;
-                    if (s % k == k - 1) {
-                        L.u1 = L.u1 + dy;
-                        L.u0 = L.u1;
                     }
                 }
+                L.a2 = fan.c2max;
                 L.ls = k * k;
             } else if (have_result) {
                 have_result = false;
@@ -1403,9 +1397,12 @@ __device__ __forceinline__ int group_scan(int v, int G, int gl, int& tot) {
 // The drain traversal.  `om`: lanes that own a query; the r-th owner's query is q[.][r] and its
 // node groups (LDS stack, then the node it was about to visit) are pool[r * PC ..].  Results go
 // back into q[.][r].
-// Returns this lane's (node visits, record tests).
-template <int NW>
-__device__ __forceinline__ uint2 coop_group_trace(const float4* __restrict__ nodes, const float4* __restrict__ tri,
+// Returns this lane's (node visits, record tests) and, in counting builds (STEPS), the wave's steps
+// with a node visit and with record tests (a step's record tests run one after the other, so a step
+// counts as many record steps as its busiest lane tests): the SIMD efficiency of tools/simd_eff.py
+// counts the lane groups' steps like the traversal loop's.
+template <int NW, bool STEPS = false>
+__device__ __forceinline__ uint4 coop_group_trace(const float4* __restrict__ nodes, const float4* __restrict__ tri,
                                                const DRefNode* __restrict__ refn, const int* __restrict__ leaf_path,
                                                int* pool, int* q, unsigned long long om, int reserve) {
     const int lane = (int)(threadIdx.x & 63);
@@ -1445,13 +1442,14 @@ __device__ __forceinline__ uint2 coop_group_trace(const float4* __restrict__ nod
         lc = (uint32_t)q[CQ_LC * COOP_Q + qi];
         lh = (uint32_t)q[CQ_LH * COOP_Q + qi];
     }
-    uint2 n{0u, 0u};
+    uint4 n{0u, 0u, 0u, 0u};
     bool done = !in_group || (any && found);
     for (;;) {
         // ---- this lane's leaf records, against the group's best at the start of the step ----
         float ct = FLT_MAX;
         int ckey = 0x7fffffff, crec = RT_NO_HIT;
         int acc_any = 0;
+        const uint32_t tests0 = n.y;
         if (!done) {
             float lt = bt;
             int lkey = bkey;
@@ -1491,6 +1489,11 @@ __device__ __forceinline__ uint2 coop_group_trace(const float4* __restrict__ nod
                 }
             }
         }
+        if (STEPS) {  // the busiest lane's record tests of this step
+            int m = (int)(n.y - tests0);
+            for (int off = 32; off > 0; off >>= 1) m = max(m, __shfl_xor(m, off));
+            n.w += (uint32_t)m;
+        }
         // ---- group reduction (aligned xor butterfly, stays inside the group) ----
         for (int off = G >> 1; off > 0; off >>= 1) {
             const float t2 = __shfl_xor(ct, off);
@@ -1525,6 +1528,7 @@ __device__ __forceinline__ uint2 coop_group_trace(const float4* __restrict__ nod
             take = max(1, min(take, (PC - reserve - top) / (NW - 1)));
         }
         const bool mine = !done && gl < take;
+        if (STEPS && __any(mine)) n.z++;
         const uint32_t item = mine ? (uint32_t)gpool[top - 1 - gl] : 0u;
         if (!done) top -= take;
         __syncthreads();
@@ -1565,7 +1569,7 @@ __device__ __forceinline__ uint2 coop_group_trace(const float4* __restrict__ nod
 // argument is wave-uniform and the call is made with every lane active (the phase-B loop's exits are
 // wave-uniform), which the lane groups' cross-lane steps need.
 template <int NW>
-__device__ __attribute__((noinline)) uint2 coop_group_trace_call(const float4* __restrict__ nodes,
+__device__ __attribute__((noinline)) uint4 coop_group_trace_call(const float4* __restrict__ nodes,
                                                                  const float4* __restrict__ tri,
                                                                  const DRefNode* __restrict__ refn,
                                                                  const int* __restrict__ leaf_path, int* pool, int* q,
@@ -1601,7 +1605,7 @@ __device__ __forceinline__ void trav_finish(const DevScene& S, Trav& T) {
 // one traversal's time instead of 64.  A sample is the same cansee query (fan_sample_query restates
 // the loop's target arithmetic for sample s); the owner resumes with the visibility mask, and in an
 // opaque scene the loop's sums are counts of visible samples, so the result is bit-identical.
-#define FAN_SLOTS 16
+#define FAN_SLOTS 8
 struct FanTable {
     int owner[FAN_SLOTS];   // lane, -1 free
     int next[FAN_SLOTS];    // next sample to hand out
@@ -1612,7 +1616,10 @@ struct FanTable {
     float hx[FAN_SLOTS], hy[FAN_SLOTS], hz[FAN_SLOTS];  // the shading point
     int plane[FAN_SLOTS];                               // 1: a plane light's k * k grid, 0: a spherical light
     unsigned long long vis[FAN_SLOTS];                  // bit s: sample s visible
+    float rx[FAN_SLOTS], ry[FAN_SLOTS], rz[FAN_SLOTS];  // plane lights: the owner's reflected direction
+    unsigned int c2max[FAN_SLOTS];                      // ... the visible samples' largest specular cosine (bits)
     float inten[FAN_SLOTS][64];                         // sample s's cansee intensity (transparent scenes)
+    float term[FAN_SLOTS][64];                          // plane lights: visible sample s's hit term
 };
 
 // Sample s of a fan (0: the centre; s >= 1: the loop's sample ls = s - 1): the cansee query of
@@ -1654,6 +1661,27 @@ __device__ __forceinline__ bool fan_sample_query(const KParams& P, v3 hp, int li
     q.d = d;
     q.t = FLT_MAX;
     return true;
+}
+
+// A visible sample s of plane-light fan f: its terms of getPlaneLights' sums (src/shadow.cpp:289-305)
+// with the loop's own arithmetic -- px reached by the loop's additions (as fan_sample_query), the owner's
+// shading point and normalize(reflect) -- so the owner's replay is a sum of finished terms in sample order
+// instead of 64 serial normalisations on one lane.  maxCos = max(0, visible samples' cosines), NaN never
+// taken: an atomic maximum of the positive cosines' bits (positive floats order as their bits).
+__device__ __forceinline__ void fan_plane_term(const KParams& P, FanTable& ft, int f, int s) {
+    const rt_plane_light pl = P.S.plane[ft.li[f]];
+    const int k = P.plane_k, i = s / k, j = s % k;
+    const v3 w = ld3(pl.width), h = ld3(pl.height);
+    const v3 dx = (1.0f / (float)(k - 1)) * w, dy = (1.0f / (float)(k - 1)) * h;
+    v3 px = ld3(pl.position);
+    for (int r = 0; r < i; ++r) px = px + dy;
+    for (int c = 0; c < j; ++c) px = px + dx;
+    const v3 hp{ft.hx[f], ft.hy[f], ft.hz[f]};
+    const v3 normal = normalize(cross(w, h));
+    const float dn = dot(normalize(hp - px), normal);
+    ft.term[f][s] = ((dn < 0.0f) ? 0.0f : dn) / length(hp - px);
+    const float c2 = dot(normalize(v3{ft.rx[f], ft.ry[f], ft.rz[f]}), normalize(px - hp));
+    if (c2 > 0.0f) atomicMax(&ft.c2max[f], __float_as_uint(c2));
 }
 
 // a sample of fan slot f finished: into the fan's mask, then its count (the owner reads the mask
@@ -1731,6 +1759,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
                 qsdist = ray_sdist;
                 atomicAdd(&ft.traced[ray_fan], 1);
             } else {
+                if (r == 1 && ft.plane[ray_fan]) fan_plane_term(P, ft, ray_fan, ray_s);
                 fan_record(ft, ray_fan, ray_s, r == 1, ray_sI);
                 ray_fan = -1;
             }
@@ -1743,6 +1772,8 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
         if (FANS && own_fan >= 0 && !tracing && !start && ft.done[own_fan] == ft.count[own_fan]) {
             fan.vis = ft.vis[own_fan];
             fan.inten = S.all_opaque ? nullptr : ft.inten[own_fan];
+            fan.term = ft.term[own_fan];
+            fan.c2max = __uint_as_float(ft.c2max[own_fan]);
             fan.done = true;
             job_rays += (uint32_t)ft.traced[own_fan];
             ft.owner[own_fan] = -1;
@@ -1800,6 +1831,10 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
                         ft.hx[f] = L.hp.x;
                         ft.hy[f] = L.hp.y;
                         ft.hz[f] = L.hp.z;
+                        ft.rx[f] = L.refl.x;
+                        ft.ry[f] = L.refl.y;
+                        ft.rz[f] = L.refl.z;
+                        ft.c2max[f] = 0u;
                         own_fan = f;
                         fan_req = false;
                     }
@@ -1838,6 +1873,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
                     ray_sdist = qsdist;
                     atomicAdd(&ft.traced[ray_fan], 1);
                 } else {  // visible without a query
+                    if (ft.plane[ray_fan]) fan_plane_term(P, ft, ray_fan, ray_s);
                     fan_record(ft, ray_fan, ray_s, true, 1.0f);
                     ray_fan = -1;
                 }
@@ -1959,15 +1995,19 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
                 if (T.cur != RT_TRAV_NONE) gp[T.sp] = (int)T.cur;
             }
             __syncthreads();
-            const uint2 nv =
+            const uint4 nv =
                 (V & RT_V_CALL) ? coop_group_trace_call<8>(S.nodes, S.tri, S.refn, S.leaf_path, coop_pool, coop_q, om,
                                                            P.coop_reserve)
-                                : coop_group_trace<8>(S.nodes, S.tri, S.refn, S.leaf_path, coop_pool, coop_q, om,
-                                                      P.coop_reserve);
+                                : coop_group_trace<8, COUNT>(S.nodes, S.tri, S.refn, S.leaf_path, coop_pool, coop_q, om,
+                                                             P.coop_reserve);
             __syncthreads();
             if (COUNT) {
                 cnt.nodes += nv.x;
                 cnt.tris += nv.y;
+                if (wave_leader()) {
+                    cnt.wnodes += nv.z;
+                    cnt.wtris += nv.w;
+                }
             }
             if (tracing) {
                 coop_get(T, coop_q, r);
@@ -2303,12 +2343,16 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
                 if (T.cur != RT_TRAV_NONE) gp[T.sp] = (int)T.cur;
             }
             __syncthreads();
-            const uint2 nv =
-                coop_group_trace<8>(S.nodes, S.tri, S.refn, S.leaf_path, coop_pool, coop_q, om, P.coop_reserve);
+            const uint4 nv =
+                coop_group_trace<8, COUNT>(S.nodes, S.tri, S.refn, S.leaf_path, coop_pool, coop_q, om, P.coop_reserve);
             __syncthreads();
             if (COUNT) {
                 cnt.nodes += nv.x;
                 cnt.tris += nv.y;
+                if (wave_leader()) {
+                    cnt.wnodes += nv.z;
+                    cnt.wtris += nv.w;
+                }
             }
             if (tracing) {
                 coop_get(T, coop_q, r);

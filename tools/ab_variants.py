@@ -27,7 +27,7 @@ DEFAULTS = {R.OPT_KERNEL: 0, R.OPT_VARIANT: -1, R.OPT_COOP: -1, R.OPT_COOP_MAX: 
 
 
 def parse(a):
-    name, kv = a.split(":", 1)
+    name, kv = a.split(":", 1) if ":" in a else (a, "")
     return name, {int(k): int(v) for k, v in (x.split("=") for x in kv.split(",") if x)}
 
 
