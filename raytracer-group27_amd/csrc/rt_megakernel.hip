@@ -1081,7 +1081,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_kernel(KParams P
 
 struct Trav {
     v3 o, d, nd, inv;
-    float thr, tcull;
+    float tcull;  // closest hit: the cull distance (the best t so far); any hit: the threshold distance - 2 eps
     Best best;
     RefMask mask;
     uint32_t cur;  // node << 8 | slot mask of the node to visit next; RT_TRAV_NONE: none
@@ -1098,7 +1098,7 @@ __device__ __forceinline__ bool leaf_pending(const Trav& T) { return T.rk > 0 ||
 // a traversal state with nothing to walk (a lane without a query this phase)
 __device__ __forceinline__ void trav_idle(Trav& T) {
     T.o = T.d = T.nd = T.inv = v3{0.0f, 0.0f, 0.0f};
-    T.thr = T.tcull = 0.0f;
+    T.tcull = 0.0f;
     T.best.t = 0.0f;
     T.best.key = -1;
     T.best.rec = RT_NO_HIT;
@@ -1119,12 +1119,12 @@ __device__ __forceinline__ void trav_init_q(const DevScene& S, bool use_bvh, v3 
     T.inv = safe_inv(qd);
     T.ref = shadow || use_bvh;
     T.any = shadow && S.all_opaque;
-    T.thr = sdist - 2.0f * 0.0005f;
+    const float thr = sdist - 2.0f * 0.0005f;
     T.best.t = qt;
     T.best.key = -1;
     T.best.rec = RT_NO_HIT;
     T.mask = RefMask{0u, 0u};
-    T.tcull = T.any ? T.thr : qt;
+    T.tcull = T.any ? thr : qt;  // an any-hit query's threshold (it never moves: the first hit ends it)
     T.found = false;
     T.sp = 0;
     T.lb = 0u;
@@ -1252,7 +1252,7 @@ __device__ __forceinline__ void trav_record(const DevScene& S, Trav& T, Cnt& cnt
     float t;
     if (!tri_test(r0, r1, r2, r3, T.o, T.d, T.nd, t)) return;
     const int key = T.ref ? __float_as_int(r3.z) : __float_as_int(r3.y);
-    if (T.any ? !(t <= T.thr) : !(t < T.best.t || (t == T.best.t && key < T.best.key))) return;
+    if (T.any ? !(t <= T.tcull) : !(t < T.best.t || (t == T.best.t && key < T.best.key))) return;
     if (T.ref && !leaf_reachable(S, __float_as_int(r3.w), T.o, T.nd, T.mask)) return;
     T.best.t = t;
     T.best.key = key;
@@ -1291,7 +1291,7 @@ __device__ __forceinline__ void coop_put(const Trav& T, int* q, int r) {
     const float f[12] = {T.o.x, T.o.y, T.o.z, T.d.x, T.d.y, T.d.z, T.nd.x, T.nd.y, T.nd.z, T.inv.x, T.inv.y, T.inv.z};
 #pragma unroll
     for (int i = 0; i < 12; ++i) q[i * COOP_Q + r] = __float_as_int(f[i]);
-    q[CQ_THR * COOP_Q + r] = __float_as_int(T.thr);
+    q[CQ_THR * COOP_Q + r] = __float_as_int(T.tcull);  // the any-hit threshold (= tcull for any-hit queries)
     q[CQ_TCULL * COOP_Q + r] = __float_as_int(T.tcull);
     q[CQ_BT * COOP_Q + r] = __float_as_int(T.best.t);
     q[CQ_BKEY * COOP_Q + r] = T.best.key;
@@ -1317,7 +1317,6 @@ __device__ __forceinline__ void coop_get(Trav& T, const int* q, int r) {
              __int_as_float(q[CQ_DZ * COOP_Q + r])};
     T.nd = v3{__int_as_float(q[CQ_NX * COOP_Q + r]), __int_as_float(q[CQ_NY * COOP_Q + r]),
               __int_as_float(q[CQ_NZ * COOP_Q + r])};
-    T.thr = __int_as_float(q[CQ_THR * COOP_Q + r]);
     T.best.t = __int_as_float(q[CQ_BT * COOP_Q + r]);
     T.best.key = q[CQ_BKEY * COOP_Q + r];
     T.best.rec = q[CQ_BREC * COOP_Q + r];
@@ -1585,7 +1584,7 @@ __device__ __forceinline__ void trav_finish(const DevScene& S, Trav& T) {
         float t;
         if (!sphere_test(sp_, T.o, T.d, t)) continue;
         const int key = T.ref ? sp_.key_bvh : S.ntri + s;
-        if (T.any ? !(t <= T.thr) : !(t < T.best.t || (t == T.best.t && key < T.best.key))) continue;
+        if (T.any ? !(t <= T.tcull) : !(t < T.best.t || (t == T.best.t && key < T.best.key))) continue;
         if (T.ref && !leaf_reachable(S, sp_.leaf, T.o, T.nd, T.mask)) continue;
         T.best.t = t;
         T.best.key = key;
@@ -2045,14 +2044,13 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
 // Its arithmetic is the general state machine's (begin_node, advance_lights_body, the forward colour
 // fold), so the image and the ray count are bit-identical (tests/test_gpu_parity.py variant matrix).
 struct LiteLane {
-    int job;        // >= 0 job; -1 idle (fetch another); -2 no more work
-    uint32_t rpix;  // the reference's pixel id y * W + x
+    int job;        // >= 0 job; -1 idle (fetch another); -2 no more work (the pixel: job_pixel)
     uint32_t sample : 7;  // camera sample
     uint32_t level : 5;   // recursion level of the current node
     uint32_t desc : 1;    // the current node descends to its mirror child after its lights
     uint32_t shadow : 1;  // the query in flight is a cansee segment
     uint32_t li : 18;     // light cursor: point lights [0, npl), then spot lights
-    v3 acc, w, wc;        // sample colour, weight of the current node, of its mirror child
+    v3 acc, w;            // sample colour, weight of the current node (its mirror child's: lite_child_weight)
     v3 hp, nN, refl;      // shading point, normalize(normal), reflect
     int mat;              // >= 0 mesh material, < 0 sphere -(s+1)
     v3 color;             // direct light of the current node
@@ -2119,6 +2117,14 @@ __device__ __forceinline__ void lite_light_visible(const KParams& P, LiteLane& L
     L.color += calc_color(lc, 1.0f, cosL, (0.0f < d2) ? d2 : 0.0f, load_mat(S, L.mat));
 }
 
+// color += ks * reflectColor (/ glossy_ray_count with shininess): the mirror child's weight from the node's
+// weight (unchanged since its begin_node) and material, evaluated when the node descends rather than kept
+__device__ __forceinline__ v3 lite_child_weight(const KParams& P, const LiteLane& L) {
+    const DMat m = load_mat(P.S, L.mat);
+    const v3 ks{m.ks[0], m.ks[1], m.ks[2]};
+    return (m.shin != 0.0f) ? L.w * ((ks * ks) / (float)P.glossy_n) : L.w * (ks * ks);
+}
+
 // The state-machine advance of the opaque-scene kernel after a finished query (q = its ray, hit / b =
 // its result): true with the next query in q (sdist: its cansee distance), false when the job is done.
 template <bool COUNT>
@@ -2148,11 +2154,7 @@ __device__ __forceinline__ bool lite_advance(const KParams& P, LiteLane& L, bool
         L.desc = false;
         if (L.level < P.max_level) {
             const v3 ks{s.m.ks[0], s.m.ks[1], s.m.ks[2]};
-            if (ks.x > 0.0f || ks.y > 0.0f || ks.z > 0.0f) {
-                L.desc = true;
-                // color += ks * reflectColor (/ glossy_ray_count with shininess): the child's weight
-                L.wc = (s.m.shin != 0.0f) ? L.w * ((ks * ks) / (float)P.glossy_n) : L.w * (ks * ks);
-            }
+            if (ks.x > 0.0f || ks.y > 0.0f || ks.z > 0.0f) L.desc = true;
         }
         node_done = true;
     } else {
@@ -2165,7 +2167,7 @@ __device__ __forceinline__ bool lite_advance(const KParams& P, LiteLane& L, bool
         }
         L.acc = L.acc + L.w * L.color;  // every light done: the node's colour, then its mirror child
         if (L.desc) {
-            L.w = L.wc;
+            L.w = lite_child_weight(P, L);
             L.level++;
             q.o = L.hp + 0.01f * L.refl;
             q.d = L.refl;
@@ -2176,7 +2178,10 @@ __device__ __forceinline__ bool lite_advance(const KParams& P, LiteLane& L, bool
     // camera sample complete
     if (store_sample(P, L.job, L.sample, L.acc)) {
         L.sample++;
-        camera_query(P, L.job, L.rpix, L.sample, q);
+        uint32_t rpix;
+        int out_row;
+        job_pixel(P, L.job, rpix, out_row);
+        camera_query(P, L.job, rpix, L.sample, q);
         L.acc = v3{0.0f, 0.0f, 0.0f};
         L.w = v3{1.0f, 1.0f, 1.0f};
         L.level = 0;
@@ -2254,9 +2259,10 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
                     if (COUNT && P.job_trace) P.job_trace[3 * job_k] = wall_clock64();
                     int out_row;
                     L.job = job_k;
-                    if (job_pixel(P, job_k, L.rpix, out_row)) {
+                    uint32_t rpix;
+                    if (job_pixel(P, job_k, rpix, out_row)) {
                         L.sample = 0;
-                        camera_query(P, job_k, L.rpix, 0, q);
+                        camera_query(P, job_k, rpix, 0, q);
                         L.acc = v3{0.0f, 0.0f, 0.0f};
                         L.w = v3{1.0f, 1.0f, 1.0f};
                         L.level = 0;
