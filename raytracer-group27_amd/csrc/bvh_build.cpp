@@ -542,7 +542,7 @@ struct Bvh2Builder {
                 }
             }
             const float leaf_cost = box.area() * n;
-            const float split_cost = 0.5f * box.area() + best;  // traversal cost ~ half a triangle
+            const float split_cost = RT_SAH_TRAVERSAL * box.area() + best;  // traversal cost ~ half a triangle
             if (best_b > 0 && (split_cost < leaf_cost || n > 2 * max_leaf)) {
                 if (par) {  // stable two-pass partition: per-chunk counts, then scatter in chunk order
                     std::vector<int> nleft(nch + 1, 0), tmp(n);

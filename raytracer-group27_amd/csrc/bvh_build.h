@@ -54,6 +54,10 @@ struct Bvh2 {
     int max_depth = 0;
 };
 
+// SAH: the cost of visiting an inner node relative to testing one triangle (both builders, bit-identical trees)
+#ifndef RT_SAH_TRAVERSAL
+#define RT_SAH_TRAVERSAL 0.5f
+#endif
 Bvh2 build_bvh2(const float* positions, int ntri, float eps, int max_leaf = 4);
 
 // Wide BVH collapsed from a Bvh2 (greedy: open the child with the largest area until `width`

@@ -746,7 +746,7 @@ __global__ __launch_bounds__(256) void k_subtrees(const STask* __restrict__ task
             const float best = __uint_as_float((uint32_t)(key >> 32));
             best_b = best < FLT_MAX ? (int)(key & 63ull) : -1;
             const float leaf_cost = box_area(E.lo, E.hi) * n;
-            const float split_cost = 0.5f * box_area(E.lo, E.hi) + best;
+            const float split_cost = RT_SAH_TRAVERSAL * box_area(E.lo, E.hi) + best;
             if (best_b > 0 && (split_cost < leaf_cost || n > 2 * kMaxLeaf)) {
                 // stable partition into idx2, then back
                 int nl = 0;
