@@ -392,7 +392,7 @@ def main():
         pmc, pmc_src = None, "not measured (--no-pmc or N > 1)"
         if world == 1 and not args.no_pmc and not args.resolution and not args.dragon_uv:
             pmc, pmc_src = measure_pmc(args.config, F, kname)
-        if pmc is None:  # the committed summary, if it was measured on this exact library build
+        if pmc is None and world == 1:  # the committed summary (one GPU's whole launch), same library build only
             pmc_c, src_c = load_pmc(pmc_key(args.config, F), kname, sha)
             if pmc_c is not None:
                 pmc, pmc_src = pmc_c, src_c
