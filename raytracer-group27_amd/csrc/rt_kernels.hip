@@ -103,6 +103,7 @@ struct KParams {
     int shade_level;            // rt_shade: recursion level of the explicit rays (getFinalColor's `level`)
     int fan;                    // dynamic-fetch kernel: bit 0 spherical-, bit 1 plane-light samples as wave-shared fans
     int interleave;             // job -> pixel: a wave's 64 jobs are one pixel of each of 64 tiles
+    int centre_first;           // job -> tile: the upper half's per-XCD tile ranges walked bottom-up (single frames)
     int fan_cap;                // ... a wave with this many pixels waiting on fans takes no new pixels
     int dual;                   // dynamic-fetch kernel: a lane testing a leaf's records also visits its next node
     uint32_t seed_lo, seed_hi;  // glossy sampling: Philox-4x32-10 key (rt_params.rng_seed)

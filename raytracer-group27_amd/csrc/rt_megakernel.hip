@@ -817,7 +817,15 @@ __device__ __forceinline__ bool job_pixel(const KParams& P, int gjob, uint32_t& 
     }
     const int tiles_x = (P.W + 7) / 8;
     const int tiles_y_band = (P.band_rows + 7) / 8;
-    const int tile = job >> 6;
+    int tile = job >> 6;
+    if (P.centre_first) {
+        // the XCD ranges of the upper half (x < 4, rows above the centre) walked from their last tile: every
+        // range starts at the rows nearest the image centre, where the long query chains are
+        const int nt = P.view_jobs >> 6;
+        int x = 7;
+        while (x > 0 && tile < ((x * nt) >> 3)) --x;
+        if (x < 4) tile = ((x * nt) >> 3) + (((x + 1) * nt) >> 3) - 1 - tile;
+    }
     const int lane = job & 63;
     const int tx = tile % tiles_x;
     const int rest = tile / tiles_x;

@@ -125,6 +125,7 @@ struct rt_ctx {
     int opt_wave_trace = 0;
     int opt_fan = 1;        // dynamic-fetch kernel: spherical-light samples as wave-shared fans
     int opt_interleave = -1;  // job -> pixel interleave: -1 by render shape, 0 off, 1 on
+    int opt_centre_first = -1;  // job -> tile: upper ranges bottom-up: -1 by render shape, 0 off, 1 on
     int opt_fan_cap = 0;      // pixels a wave may have waiting on fans before it stops taking new ones (0: default)
     int opt_dual = -1;        // dynamic-fetch steps: record and node visit in one iteration (-1 default, 0 off, 1 on)
     int opt_variant = -1;   // -1: the shipped variant for the render shape (RT_DF_BATCH / _FRAME, RT_WT_DEFAULT)
@@ -810,6 +811,10 @@ static int set_option_one(rt_ctx* c, int option, int value) {
             if (value < -1 || value > 1) break;
             c->opt_interleave = value;
             return RT_OK;
+        case RT_OPT_CENTRE_FIRST:
+            if (value < -1 || value > 1) break;
+            c->opt_centre_first = value;
+            return RT_OK;
         case RT_OPT_DUAL_STEP:
             if (value < -1 || value > 1) break;
             c->opt_dual = value;
@@ -1136,6 +1141,10 @@ static void shape_options(const rt_ctx* c, KParams& K) {
     // single frames with fans: a wave's jobs spread over 64 tiles (C4 52.9 -> 31.4 ms; the tile order
     // keeps its coherence elsewhere: C3 2.18 vs 2.41 ms, C2 0.77 vs 0.98 ms)
     K.interleave = c->opt_interleave >= 0 ? c->opt_interleave : (K.fan && K.n_views <= 1 ? 1 : 0);
+    // single frames of the opaque-scene kernel start every XCD range at its rows nearest the image centre: the
+    // frame's longest query chains (reflections inside the object) start first (C3 frame 1.40 -> 1.33 ms; the
+    // 64-view batch and the fan renders, C4 / C5, gain nothing or lose: DESIGN.md section 6c)
+    K.centre_first = c->opt_centre_first >= 0 ? c->opt_centre_first : (K.n_views <= 1 && opaque_path(c, K, true) ? 1 : 0);
     // fan renders advance whole waves: the fans keep a wave's free lanes busy, so waiting for all 64
     // costs little and each pass takes many new pixels (C4 single frame, refill 24 -> 64: 27.0 -> 13.2 ms)
     if (K.fan && c->opt_refill == 0) K.refill = 64;

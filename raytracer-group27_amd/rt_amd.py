@@ -152,6 +152,7 @@ def set_build_mode(mode):
 OPT_KERNEL, OPT_COOP, OPT_COOP_MAX, OPT_REFILL, OPT_WAVE_TRACE, OPT_VARIANT, OPT_FAN, OPT_INTERLEAVE, OPT_FAN_CAP = \
     1, 2, 3, 4, 5, 6, 7, 8, 9
 OPT_DUAL_STEP = 10
+OPT_CENTRE_FIRST = 12  # job order: upper-half XCD tile ranges walked bottom-up (-1 by shape, 0 off, 1 on)
 OPT_OPAQUE = 11  # opaque-scene kernel: -1 where eligible (default), 0 the general kernels, 1 / 2 the 4- / 3-wave build
 KERNEL_AUTO, KERNEL_WHOLE_TRAVERSAL, KERNEL_DYNAMIC_FETCH = 0, 1, 2
 # compiled kernel variants (rt_megakernel.hip RT_V_*, rt_runtime.hip RT_DF_* / RT_WT_*)

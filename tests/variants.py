@@ -6,7 +6,8 @@ import contextlib
 
 def defaults(R):
     return {R.OPT_KERNEL: R.KERNEL_AUTO, R.OPT_VARIANT: -1, R.OPT_COOP: -1, R.OPT_COOP_MAX: 0, R.OPT_REFILL: 0,
-            R.OPT_FAN: 1, R.OPT_INTERLEAVE: -1, R.OPT_FAN_CAP: 0, R.OPT_DUAL_STEP: -1, R.OPT_OPAQUE: -1}
+            R.OPT_FAN: 1, R.OPT_INTERLEAVE: -1, R.OPT_FAN_CAP: 0, R.OPT_DUAL_STEP: -1, R.OPT_OPAQUE: -1,
+            R.OPT_CENTRE_FIRST: -1}
 
 
 def kernel_classes(R):
@@ -27,6 +28,7 @@ def all_variants(R):
         {R.OPT_KERNEL: df, R.OPT_VARIANT: R.DF_BATCH, R.OPT_FAN: 0},
         {R.OPT_KERNEL: df, R.OPT_INTERLEAVE: 1, R.OPT_FAN: 0},  # a wave's pixels spread over 64 tiles
         {R.OPT_KERNEL: df, R.OPT_INTERLEAVE: 0},
+        {R.OPT_KERNEL: df, R.OPT_CENTRE_FIRST: 1},              # upper-half tile ranges walked bottom-up
         {R.OPT_KERNEL: wt, R.OPT_INTERLEAVE: 1},
         {R.OPT_KERNEL: df, R.OPT_DUAL_STEP: 0},                 # one record or one node visit per step
         {R.OPT_KERNEL: df, R.OPT_VARIANT: R.DF_BATCH, R.OPT_DUAL_STEP: 0},
