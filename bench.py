@@ -35,6 +35,8 @@ import numpy as np  # noqa: E402
 
 METRIC = "Mrays/s (primary+shadow+secondary) at 1920×1080; fraction of HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+# VALU issue peak: 256 CUs x 4 SIMDs x 2.4 GHz / 4 cycles per wave64 VALU instruction
+VALU_PEAK_WAVE_INSTR_S = 256 * 4 * 2.4e9 / 4
 BAND_ROWS = 8
 DEFAULT_VIEWS = 64  # frames per step: a 64-view turntable (5.625 deg apart) of the C3 scene in one launch
 # frames per step of the other configs (a step of a few hundred ms at most): C4's 64-sample soft shadows
@@ -125,11 +127,12 @@ def pmc_key(config, views):
 
 
 def measure_pmc(config, views, kernel, timeout_s=150):
-    """HBM bytes per render launch measured now: two rocprofv3 --pmc passes (FETCH_SIZE, then WRITE_SIZE:
-    together they exceed the 4 TCC counters one pass can hold) over tools/prof_target.py, which makes the
-    same launches this bench times (config, views, library); per MI355X_MICROARCH.md's HBM section
-    FETCH_SIZE and WRITE_SIZE are KB and gfx950's FETCH_SIZE tallies 128-B requests at 64 B, so
-    bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.  Returns (bytes or None, provenance)."""
+    """HBM bytes and VALU instructions per render launch measured now: three rocprofv3 --pmc passes
+    (FETCH_SIZE, WRITE_SIZE -- together they exceed the 4 TCC counters one pass can hold -- and
+    SQ_INSTS_VALU) over tools/prof_target.py, which makes the same launches this bench times (config,
+    views, library); per MI355X_MICROARCH.md's HBM section FETCH_SIZE and WRITE_SIZE are KB and gfx950's
+    FETCH_SIZE tallies 128-B requests at 64 B, so bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.
+    Returns (bytes or None, provenance, {counter: median per launch})."""
     import shutil
     import subprocess
     import tempfile
@@ -139,26 +142,26 @@ def measure_pmc(config, views, kernel, timeout_s=150):
 
     exe = shutil.which("rocprofv3")
     if not exe:
-        return None, "rocprofv3 not found"
+        return None, "rocprofv3 not found", {}
     med = {}
     with tempfile.TemporaryDirectory(prefix="bench_pmc_") as tmp:
-        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU"):
             out = os.path.join(tmp, ctr)
             cmd = ["timeout", "-s", "KILL", str(timeout_s), exe, "--pmc", ctr, "--kernel-trace", "--output-format", "csv",
                    "-d", out, "-o", "run", "--", sys.executable, os.path.join(REPO, "tools", "prof_target.py"),
                    config, "2", str(views)]
             r = subprocess.run(cmd, capture_output=True, text=True, cwd=REPO)
             if r.returncode != 0:
-                return None, f"rocprofv3 --pmc {ctr} failed (rc {r.returncode}): {(r.stderr or r.stdout)[-300:]}"
+                return None, f"rocprofv3 --pmc {ctr} failed (rc {r.returncode}): {(r.stderr or r.stdout)[-300:]}", med
             kname, m = pmc_summary.collect(out)
             if ctr not in m or not kname or kernel not in kname:
-                return None, f"rocprofv3 --pmc {ctr}: no counter rows for {kernel}"
+                return None, f"rocprofv3 --pmc {ctr}: no counter rows for {kernel}", med
             med[ctr] = m[ctr]
     hbm = (2.0 * med["FETCH_SIZE"] + med["WRITE_SIZE"]) * 1024.0
     return hbm, (f"measured in this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over tools/prof_target.py "
                  f"{config} {views} views (the same kernel and library), median per launch; FETCH_SIZE "
                  f"{med['FETCH_SIZE']:.0f} KB (x2, gfx950 64-B tally of 128-B requests), WRITE_SIZE "
-                 f"{med['WRITE_SIZE']:.0f} KB")
+                 f"{med['WRITE_SIZE']:.0f} KB"), med
 
 
 def load_pmc(config, kernel, sha, path=None):
@@ -191,15 +194,18 @@ def main():
                     help="skip the single-frame latency record (profiling runs: one kernel shape only)")
     ap.add_argument("--partition", choices=("bands", "frames"), default="bands",
                     help="N>1: bands = every view of the step split into interleaved 8-row bands over the ranks, "
-                         "RCCL gather to rank 0, un-permute there (north_star's tile split, strong scaling); frames = "
-                         "every rank renders its own turntable views (weak scaling, no collective on the data path)")
+                         "the pixels exchanged into rank 0's images as --exchange says (north_star's tile split, strong "
+                         "scaling); frames = every rank renders its own turntable views (weak scaling, no collective "
+                         "on the data path)")
     ap.add_argument("--views", type=int, default=None,
                     help="frames per step, rendered in ONE launch (default per config: C3 64, C4 16, C5 2)")
     ap.add_argument("--view-step", type=float, default=None,
                     help="turntable step between views in degrees (default 360 / views)")
-    ap.add_argument("--exchange", choices=("ipc", "gather"), default="ipc",
+    ap.add_argument("--exchange", choices=("ipc", "gather", "none"), default="ipc",
                     help="N>1 bands: ipc = every rank stores its pixels straight into rank 0's images (IPC-mapped, "
-                         "no gather step); gather = band buffers + RCCL gather + un-permute on rank 0")
+                         "no gather step); gather = band buffers + RCCL gather + un-permute on rank 0; none = the "
+                         "control leg: every rank stores its bands into its OWN images (the same render work with no "
+                         "exchange, so a scaling run can separate the exchange's cost)")
     ap.add_argument("--cpu-pixels", type=int, default=0,
                     help="CPU baseline: stop each leg at this many pixels as well as at --cpu-budget (0: budget only)")
     ap.add_argument("--resolution", default=None, help="WxH override (tests; the BENCH line uses the config's)")
@@ -258,18 +264,30 @@ def main():
     exchange = "local" if (world == 1 or not bands) else args.exchange
     ipc = None
     if exchange == "ipc":
-        # rank 0's images, opened by every other rank: the ranks' kernels store their pixels into them
-        try:
-            if rank == 0:
+        # rank 0's images, opened by every other rank: the ranks' kernels store their pixels into them.  Every
+        # rank takes part in the broadcast whatever rank 0's allocation did (None: no buffer), so a failure on
+        # any rank falls back to the gather scheme instead of leaving the ranks in mismatched collectives.
+        ok, handle = 1, None
+        if rank == 0:
+            try:
+                if os.environ.get("BENCH_IPC_FAIL_RANK0"):  # test hook: rank 0's export fails
+                    raise R.RtError("rt_ipc_alloc: forced failure (BENCH_IPC_FAIL_RANK0)")
                 ipc = R.IpcBuffer(local, nbytes=img_elems * 4)
-            obj = [ipc.handle if rank == 0 else None]
-            dist.broadcast_object_list(obj, src=0)
-            if rank != 0:
-                ipc = R.IpcBuffer(local, handle=obj[0])
-            ok = 1
-        except R.RtError as e:  # no IPC on this node: the gather scheme
-            print(f"rank {rank}: IPC mapping failed ({e}); falling back to --exchange gather", file=sys.stderr)
-            ok = 0
+                handle = ipc.handle
+            except R.RtError as e:
+                print(f"rank 0: IPC export failed ({e}); falling back to --exchange gather", file=sys.stderr)
+                ok = 0
+        obj = [handle]
+        dist.broadcast_object_list(obj, src=0)
+        if rank != 0:
+            if obj[0] is None:
+                ok = 0
+            else:
+                try:
+                    ipc = R.IpcBuffer(local, handle=obj[0])
+                except R.RtError as e:  # no IPC on this node: the gather scheme
+                    print(f"rank {rank}: IPC mapping failed ({e}); falling back to --exchange gather", file=sys.stderr)
+                    ok = 0
         flag = torch.tensor([ok], dtype=torch.int32, device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         if not int(flag.item()):
@@ -277,6 +295,7 @@ def main():
                 ipc.close()
             ipc = None
             exchange = "gather"
+    # (exchange "none": every rank's own images, the control leg; "local": N = 1 or frames)
     images = None if exchange == "ipc" else torch.zeros(img_elems, dtype=torch.float32, device=dev)
     img_ptr = ipc.ptr if exchange == "ipc" else images.data_ptr()
     nbands = (H + BAND_ROWS - 1) // BAND_ROWS
@@ -389,9 +408,9 @@ def main():
         achieved = bytes0 / (avg_ms * 1e-3) / 1e9
         kname = st.kernel_name
         sha = lib_sha()
-        pmc, pmc_src = None, "not measured (--no-pmc or N > 1)"
+        pmc, pmc_src, pmc_med = None, "not measured (--no-pmc or N > 1)", {}
         if world == 1 and not args.no_pmc and not args.resolution and not args.dragon_uv:
-            pmc, pmc_src = measure_pmc(args.config, F, kname)
+            pmc, pmc_src, pmc_med = measure_pmc(args.config, F, kname)
         if pmc is None and world == 1:  # the committed summary (one GPU's whole launch), same library build only
             pmc_c, src_c = load_pmc(pmc_key(args.config, F), kname, sha)
             if pmc_c is not None:
@@ -419,6 +438,8 @@ def main():
                        "partition": (f"{world}-GPU tile split: interleaved 8-row bands of every view, "
                                      + ("each rank's pixels stored straight into rank 0's images (IPC-mapped, "
                                         "stores over xGMI while rendering; no gather step)" if exchange == "ipc" else
+                                        "NO exchange (control leg: each rank stores its bands into its own images)"
+                                        if exchange == "none" else
                                         "RCCL gather to rank 0 + un-permute" if to_root else
                                         f"{dist.get_backend()} all-gather + un-permute")
                                      if bands and world > 1 else
@@ -438,11 +459,26 @@ def main():
                          "kernel": kname, "lib_sha": sha, "kernel_avg_ms": avg_ms,
                          "algorithmic_bytes_per_launch": int(bytes0)},
         }
+        if "SQ_INSTS_VALU" in pmc_med:
+            # the VALU issue roofline beside SURVEY.md §8d's algorithmic-byte one: the kernels are branchy scalar
+            # FP32 whose bytes come mostly from L2 / MALL, so the issue rate is usually the binding limit;
+            # "bound" names whichever fraction is higher (achieved / peak / frac above stay the HBM figures)
+            vi = float(pmc_med["SQ_INSTS_VALU"])
+            ia = vi / (avg_ms * 1e-3)
+            line["roofline"]["issue"] = {
+                "achieved": ia, "peak": VALU_PEAK_WAVE_INSTR_S, "unit": "wave-instructions/s",
+                "frac": ia / VALU_PEAK_WAVE_INSTR_S, "valu_insts_per_launch": vi,
+                "valu_insts_per_ray": vi / max(1.0, float(cst.rays)),
+                "source": "rocprofv3 --pmc SQ_INSTS_VALU (median per launch, same run) / kernel_avg_ms; peak = 256 CUs "
+                          "x 4 SIMDs x 2.4 GHz / 4 cycles per wave64 VALU instruction"}
+            if ia / VALU_PEAK_WAVE_INSTR_S > achieved / HBM_PEAK_GBS:
+                line["roofline"]["bound"] = "valu-issue"
         if single is not None:
             line["single_frame"] = single
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.config, budget_s=args.cpu_budget, max_pixels=args.cpu_pixels or None)
         print(json.dumps(line), flush=True)
+    ctx.close()  # explicitly: no HIP teardown left to interpreter exit
     if ipc is not None and not ipc.owner:  # the importers unmap rank 0's images before rank 0 frees them
         ipc.close()
     if world > 1:

@@ -278,10 +278,15 @@ int rt_camera_from_trackball(const float look_at[3], const float euler_radians[3
  * one of the two runtimes without a device). */
 int rt_device_count(int* n);
 /* BoundingVolumeHierarchy(Scene*) over devices[0..ndev): a whole scene replica (acceleration structures
- * built on that device) per entry, peer access from every other device to devices[0]. */
+ * built on that device) per entry, peer access from every other device to devices[0] where the node has
+ * it.  A device without peer access does not fail the create: its part of every split render is rendered
+ * band-dense on that device and copied to devices[0] (hipMemcpyPeerAsync + one scatter launch). */
 int rt_create(const rt_scene_desc* desc, const int* devices, int ndev, rt_ctx** out);
 /* The context's device list into out (up to n entries); returns ndev. */
 int rt_ctx_devices(rt_ctx* ctx, int* out, int n);
+/* Per replica: 1 if its kernels store pixels straight into devices[0]'s images (peer access), 0 if it
+ * renders band-dense and copies (no peer access, or RT_OPT_PEER_STORES 0); returns ndev. */
+int rt_ctx_peer_stores(rt_ctx* ctx, int* out, int n);
 int rt_destroy(rt_ctx* ctx);
 
 /* Whole frame to host memory: rgb_out = W*H*3 floats in Screen::m_textureData order (every device of
@@ -376,6 +381,8 @@ int rt_debug_counters(rt_ctx* ctx, uint64_t* out, int n);
 #define RT_OPT_DUAL_STEP 10  /* dynamic-fetch kernel: a lane testing leaf records also visits its next node in the same step (-1 default = 1, 0 off) */
 #define RT_OPT_CENTRE_FIRST 12 /* job order: the per-XCD tile ranges above the image centre walked bottom-up, so every range starts at its rows nearest the centre: -1 by render shape, 0 off, 1 on */
 #define RT_OPT_OPAQUE 11     /* opaque-scene kernel (opaque materials, point / spot lights, no lobes or textures): -1 where eligible (4 waves/SIMD for view batches, 3 for single frames), 0 never, 1 / 2 force the 4- / 3-wave build */
+#define RT_OPT_TREE 13       /* recursion-tree kernel (transparent materials, all four light types with <= 64-sample fans, no lobes or textures): -1 where eligible, 0 never, 1 / 2 force the 4- / 3-wave build */
+#define RT_OPT_PEER_STORES 14 /* split renders: -1 the replicas with peer access to devices[0] store their pixels straight into its images (default), 0 every replica renders band-dense on its own device and copies (the path of devices without peer access) */
 #define RT_KERNEL_AUTO 0
 #define RT_KERNEL_WHOLE_TRAVERSAL 1
 #define RT_KERNEL_DYNAMIC_FETCH 2

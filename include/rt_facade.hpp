@@ -391,7 +391,7 @@ public:
         d.spheres = sph.data();
         d.num_textures = (int)texs.size();
         d.textures = texs.data();
-        lights_of(sc, d);
+        lights_of(sc, lights_, d);
         check(rt_create(&d, devices.data(), (int)devices.size(), &ctx_), "BoundingVolumeHierarchy");
         mesh_tex_.clear();
         for (const rt_material& m : mats) mesh_tex_.push_back(m.texture);
@@ -442,17 +442,23 @@ public:
     void sync(const Scene& sc) const {
         if (sc.meshes.size() != synced_mats_.size() || sc.spheres.size() != synced_sph_.size())
             throw std::runtime_error("BoundingVolumeHierarchy: the scene's geometry changed; build a new one");
+        // the new arrays are built aside and become the pushed copies only once the device has them: a
+        // failed update throws and leaves the copies as they were, so the next sync() retries it
         if (lights_changed(sc)) {
             rt_scene_desc d{};
-            lights_of(sc, d);
+            Lights fresh;
+            lights_of(sc, fresh, d);
             check(rt_update_lights(ctx_, &d), "rt_update_lights");
+            lights_ = std::move(fresh);
         }
         if (materials_changed(sc)) {
-            for (size_t i = 0; i < sc.meshes.size(); ++i) synced_mats_[i] = detail::c_material(sc.meshes[i].material, mesh_tex_[i]);
-            for (size_t i = 0; i < sc.spheres.size(); ++i) synced_sph_[i] = detail::c_material(sc.spheres[i].material, -1);
-            check(rt_update_materials(ctx_, (int)synced_mats_.size(), synced_mats_.data(), (int)synced_sph_.size(),
-                                      synced_sph_.data()),
+            std::vector<rt_material> mats(sc.meshes.size()), sph(sc.spheres.size());
+            for (size_t i = 0; i < sc.meshes.size(); ++i) mats[i] = detail::c_material(sc.meshes[i].material, mesh_tex_[i]);
+            for (size_t i = 0; i < sc.spheres.size(); ++i) sph[i] = detail::c_material(sc.spheres[i].material, -1);
+            check(rt_update_materials(ctx_, (int)mats.size(), mats.data(), (int)sph.size(), sph.data()),
                   "rt_update_materials");
+            synced_mats_ = std::move(mats);
+            synced_sph_ = std::move(sph);
         }
     }
     // getFinalColor's per-call sync (default on, the reference's semantics); off: the caller syncs
@@ -498,9 +504,16 @@ private:
         }
         return false;
     }
+    // the lights last pushed to the device, in the C-ABI's structs
+    struct Lights {
+        std::vector<rt_point_light> pl;
+        std::vector<rt_spherical_light> sl;
+        std::vector<rt_spot_light> sp;
+        std::vector<rt_plane_light> pn;
+    };
     bool lights_changed(const Scene& sc) const {
-        return differs(sc.pointLights, l_pl_) || differs(sc.sphericalLight, l_sl_) || differs(sc.spotLight, l_sp_) ||
-               differs(sc.planeLight, l_pn_);
+        return differs(sc.pointLights, lights_.pl) || differs(sc.sphericalLight, lights_.sl) ||
+               differs(sc.spotLight, lights_.sp) || differs(sc.planeLight, lights_.pn);
     }
     bool materials_changed(const Scene& sc) const {
         for (size_t i = 0; i < sc.meshes.size(); ++i) {
@@ -513,34 +526,28 @@ private:
         }
         return false;
     }
-    // the scene's lights into the pushed copies l_*_ and d's pointers to them
-    void lights_of(const Scene& sc, rt_scene_desc& d) const {
-        l_pl_.clear();
-        l_sl_.clear();
-        l_sp_.clear();
-        l_pn_.clear();
-        for (const PointLight& l : sc.pointLights) l_pl_.push_back(conv(l));
-        for (const SphericalLight& l : sc.sphericalLight) l_sl_.push_back(conv(l));
-        for (const SpotLight& l : sc.spotLight) l_sp_.push_back(conv(l));
-        for (const PlaneLight& l : sc.planeLight) l_pn_.push_back(conv(l));
-        d.num_point_lights = (int)l_pl_.size();
-        d.point_lights = l_pl_.data();
-        d.num_spherical_lights = (int)l_sl_.size();
-        d.spherical_lights = l_sl_.data();
-        d.num_spot_lights = (int)l_sp_.size();
-        d.spot_lights = l_sp_.data();
-        d.num_plane_lights = (int)l_pn_.size();
-        d.plane_lights = l_pn_.data();
+    // the scene's lights into `out` and d's pointers to them
+    static void lights_of(const Scene& sc, Lights& out, rt_scene_desc& d) {
+        out = Lights{};
+        for (const PointLight& l : sc.pointLights) out.pl.push_back(conv(l));
+        for (const SphericalLight& l : sc.sphericalLight) out.sl.push_back(conv(l));
+        for (const SpotLight& l : sc.spotLight) out.sp.push_back(conv(l));
+        for (const PlaneLight& l : sc.planeLight) out.pn.push_back(conv(l));
+        d.num_point_lights = (int)out.pl.size();
+        d.point_lights = out.pl.data();
+        d.num_spherical_lights = (int)out.sl.size();
+        d.spherical_lights = out.sl.data();
+        d.num_spot_lights = (int)out.sp.size();
+        d.spot_lights = out.sp.data();
+        d.num_plane_lights = (int)out.pn.size();
+        d.plane_lights = out.pn.data();
     }
 
     Scene* scene_ = nullptr;
     rt_ctx* ctx_ = nullptr;
     std::vector<int> mesh_tex_;
     mutable std::vector<rt_material> synced_mats_, synced_sph_;
-    mutable std::vector<rt_point_light> l_pl_;
-    mutable std::vector<rt_spherical_light> l_sl_;
-    mutable std::vector<rt_spot_light> l_sp_;
-    mutable std::vector<rt_plane_light> l_pn_;
+    mutable Lights lights_;
     bool auto_sync_ = true;
 };
 

@@ -116,6 +116,10 @@ struct KParams {
     // camera at views[12 v] (cam xyz, quat wxyz, hh, hw), its rows at out + v * view_rows * W * 3
     int n_views, view_jobs, view_rows;
     const float* views;
+    // recursion-tree kernel: the lanes' pending refracted rays, frame f of lane slot s (= block * 64 + lane)
+    // at frames + (f * frame_slots + s) * 3 (3 float4: origin + child level, direction, weight)
+    float4* frames;
+    int frame_slots;
 };
 
 // Philox-4x32-10 (Salmon et al., SC'11; the Random123 constants): the counter-based stream that
@@ -612,6 +616,27 @@ __global__ void unpermute_views_kernel(int W, int H, int band_rows, int band_cou
     const int lb = gb / band_count;
     const float* s = src + (((((size_t)rank * n_views + v) * max_local + lb) * band_rows + r) * W + x) * 3;
     float* d = dst + ((size_t)v * per_view + (size_t)(H - 1 - y) * W + x) * 3;
+    d[0] = s[0];
+    d[1] = s[1];
+    d[2] = s[2];
+}
+
+// One rank's band-dense buffer [n_views][max_local][band_rows][W][3] (rank of count: its local band lb is
+// the frame's band lb * count + rank) -> its rows of the n_views images in the setPixel layout.
+__global__ void scatter_bands_kernel(int W, int H, int band_rows, int rank, int count, int max_local, int n_views,
+                                     const float* src, float* dst) {
+    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t per_view = (size_t)max_local * band_rows * W;
+    if (idx >= per_view * n_views) return;
+    const int v = (int)(idx / per_view);
+    const size_t k = idx - (size_t)v * per_view;
+    const int x = (int)(k % W);
+    const int r = (int)(k / W);  // row of the rank's band-dense view
+    const int lb = r / band_rows, row = r % band_rows;
+    const int y = (lb * count + rank) * band_rows + row;
+    if (y >= H) return;
+    const float* s = src + idx * 3;
+    float* d = dst + ((size_t)v * H * W + (size_t)(H - 1 - y) * W + x) * 3;
     d[0] = s[0];
     d[1] = s[1];
     d[2] = s[2];

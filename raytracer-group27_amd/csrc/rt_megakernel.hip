@@ -2394,6 +2394,525 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
 #undef RT_FRESH
 }
 
+// ---- the recursion-tree kernel: transparent materials and every light type, lane state in registers ----
+// getFinalColor (src/main.cpp:129-301) on any scene without glossy lobes (glossy_ray_count == 1, or no
+// glossy material) and without textures, whose spherical and plane lights take at most 64 samples: the C4
+// and C5 configurations.  It is the opaque kernel's inline, register-resident state machine extended with
+//   * the transparent reflect + refract tree (src/main.cpp:257-290): the reflected child is walked at once,
+//     the refracted one is a pending frame on a per-lane stack in device memory (48 B, written only when a
+//     transparent node is shaded: the stack is depth-first, so it never holds more than max_level frames);
+//   * the cansee segment loop past transparent surfaces (src/shadow.cpp:41-67) for point and spot lights;
+//   * spherical and plane lights as wave-shared fans (FanTable, as in persistent_df_kernel): the owner posts
+//     the light, the wave's free lanes trace its samples, the owner folds their results in sample order.
+// The general state machine keeps a 42-dword lane image and its frames in private memory around an
+// out-of-line call (C5: ~170 GB of scratch writes per 4K frame); here the ~26 dwords below stay in VGPRs.
+// Every expression is the general machine's (begin_node, advance_lights_body, next_branch, cansee_step,
+// the fan folds), so images and ray counts are bit-identical (tests/test_gpu_parity.py variant matrix).
+struct TreeLane {
+    int job;               // >= 0 job; -1 idle; -2 no more work
+    uint32_t sample : 6;   // camera sample (< 64)
+    uint32_t level : 4;    // recursion level of the current node (max_level < 16)
+    uint32_t desc : 1;     // the current node descends to its mirror / reflected child after its lights
+    uint32_t shadow : 1;   // the lane's own query in flight is a cansee segment (point / spot light)
+    uint32_t nfr : 4;      // pending refracted rays on the lane's frame stack
+    uint32_t li : 16;      // light cursor over point, spherical, spot, then plane lights (getFinalColor's order)
+    v3 acc, w;             // sample colour; weight of the current node
+    v3 hp, nN, refl;       // shading point, normalize(normal), reflect
+    int mat;               // >= 0 mesh material, < 0 sphere -(s+1)
+    v3 color;              // direct light of the current node
+    float rc;              // transparent node: the reflected child's Fresnel weight R
+};
+
+// one refracted ray pending on the lane's stack (the general machine's FR_REFRACT frame)
+__device__ __forceinline__ float4* tree_frame(const KParams& P, int f) {
+    return P.frames + ((size_t)f * P.frame_slots + blockIdx.x * RT_WAVE + (threadIdx.x & 63)) * 3;
+}
+
+// a point or spot light under the cursor was visible with cansee intensity sI: its calcColor
+__device__ __forceinline__ void tree_light_visible(const KParams& P, TreeLane& L, float sI) {
+    const DevScene& S = P.S;
+    v3 lp, lc;
+    if ((int)L.li < S.npl) {
+        const rt_point_light pl = S.pl[L.li];
+        lp = ld3(pl.position);
+        lc = ld3(pl.color);
+    } else {
+        const DSpot sp = S.spot[L.li - S.npl - S.nsl];
+        lp = ld3(sp.pos);
+        lc = ld3(sp.color);
+    }
+    const v3 ldir = normalize(lp - L.hp);
+    const float cosL = fabsf(dot(L.nN, ldir));
+    const float d2 = dot(normalize(L.refl), ldir);
+    L.color += calc_color(lc, sI, cosL, (0.0f < d2) ? d2 : 0.0f, load_mat(S, L.mat));
+}
+
+// A finished fan of the spherical or plane light under the cursor: getSpherelights' / getPlaneLights' sums
+// replayed in sample order from the samples' visibility, intensities and (plane) hit terms, as
+// advance_lights_body folds them (src/shadow.cpp:145-226, 255-321).
+__device__ __forceinline__ void tree_fan_light(const KParams& P, TreeLane& L, const FanResult& fan) {
+    const DevScene& S = P.S;
+    const DMat m = load_mat(S, L.mat);
+    const int li = (int)L.li;
+    if (li < S.npl + S.nsl) {
+        const rt_spherical_light sl = S.sl[li - S.npl];
+        float a0, a1;
+        if (!fan.inten) {
+            const float nv = (float)__popcll(fan.vis >> 1);
+            a0 = 1.0f + nv;
+            a1 = (float)(fan.vis & 1ull) + nv;
+        } else {
+            a0 = fan.inten[0];
+            a1 = (fan.vis & 1ull) ? 1.0f : 0.0f;
+            for (int s = 1; s <= P.sl_m * P.sl_n; ++s)
+                if ((fan.vis >> s) & 1ull) {
+                    a1 += 1.0f;
+                    a0 += fan.inten[s];
+                }
+        }
+        if (a1 > 0.0f) {
+            const v3 ldir = normalize(ld3(sl.position) - L.hp);
+            const float cosL = fabsf(dot(L.nN, ldir));
+            const float d2 = dot(normalize(L.refl), ldir);
+            L.color += calc_color(ld3(sl.color), a0 / (float)P.sl_count, cosL, (0.0f < d2) ? d2 : 0.0f, m);
+        }
+    } else {
+        const rt_plane_light pl = S.plane[li - S.npl - S.nsl - S.nspot];
+        const int k = P.plane_k;
+        float a0 = 0.0f, a1 = 0.0f, a3 = 0.0f;
+        for (int s = 0; s < k * k; ++s)
+            if ((fan.vis >> s) & 1ull) {
+                a3 += fan.inten ? fan.inten[s] : 1.0f;
+                a0 += fan.term[s];
+                a1 += 1.0f;
+            }
+        if (a0 > 0.0f) {
+            const float lin = (a3 / (float)(int)a1) * a0 / (float)(k * k);
+            L.color += calc_color(ld3(pl.color), lin, 1.0f, fan.c2max, m);
+        }
+    }
+}
+
+// The next light of the cursor that needs work: 1 = the lane's own cansee segment (point / spot light)
+// queued in q with its distance and intensity; 2 = a fan to post (spherical light, or a plane light the
+// shading point is in front of); 0 = the node's lights are done.  Lights visible without a query
+// (target within SHADOW_ERROR_OFFSET) count at once; spot lights outside their cone and plane lights
+// behind the point contribute nothing (src/shadow.cpp:235-237, 270-272).
+__device__ __forceinline__ int tree_next_light(const KParams& P, TreeLane& L, Query& q, float& sdist, float& sI) {
+    const DevScene& S = P.S;
+    const int n_ps = S.npl + S.nsl, n_pss = n_ps + S.nspot, nl = n_pss + S.nplane;
+    while ((int)L.li < nl) {
+        const int li = (int)L.li;
+        if (li >= S.npl && li < n_ps) return 2;
+        if (li >= n_pss) {
+            const rt_plane_light pl = S.plane[li - n_pss];
+            const v3 w = ld3(pl.width), h = ld3(pl.height), lpos = ld3(pl.position);
+            const v3 normal = normalize(cross(w, h));
+            if (dot(normalize(L.hp - (lpos + 0.5f * (w + h))), normal) > 0.0f) return 2;
+            L.li++;
+            continue;
+        }
+        v3 lp;
+        if (li < S.npl) {
+            lp = ld3(S.pl[li].position);
+        } else {
+            const DSpot sp = S.spot[li - n_ps];
+            lp = ld3(sp.pos);
+            if (!(dot(normalize(ld3(sp.dir)), normalize(L.hp - lp)) > sp.cos_angle)) {
+                L.li++;
+                continue;
+            }
+        }
+        v3 d = lp - L.hp;  // start_cansee
+        sdist = length(d);
+        d = normalize(d);
+        sI = 1.0f;
+        if (sdist > 0.0005f) {
+            q.o = L.hp + 0.0005f * d;
+            q.d = d;
+            q.t = FLT_MAX;
+            return 1;
+        }
+        tree_light_visible(P, L, 1.0f);
+        L.li++;
+    }
+    return 0;
+}
+
+enum { TA_DONE = 0, TA_QUERY = 1, TA_FAN = 2 };
+
+// The tree kernel's advance after a finished query or fan: `vis` = the lane's own cansee result (its
+// shadow query ended: 1 visible, 0 blocked), `fan` = the completed fan of the light under the cursor,
+// else the path query (q = its ray, hit / b = its result) ended.  TA_QUERY with the next query in q
+// (sdist / sI: a cansee segment's distance and intensity), TA_FAN when a fan is to be posted, TA_DONE when
+// the job is complete.
+template <bool COUNT>
+__device__ __forceinline__ int tree_advance(const KParams& P, TreeLane& L, int vis, const FanResult& fan, bool hit,
+                                            const Best& b, Query& q, float& sdist, float& sI, Cnt& cnt) {
+    const DevScene& S = P.S;
+    bool node_done = true;
+    if (fan.done) {
+        tree_fan_light(P, L, fan);
+        L.li++;
+    } else if (L.shadow) {
+        if (vis) tree_light_visible(P, L, sI);
+        L.li++;
+        L.shadow = false;
+    } else if (hit) {
+        // begin_node (src/main.cpp:131-290)
+        const Surf s = surface(S, q.o, q.d, b, false, L.level == 0);
+        if (COUNT) {
+            cnt.hits++;
+            if (s.ub) cnt.ub++;
+        }
+        L.hp = s.p;
+        L.nN = normalize(s.n);
+        L.refl = reflect(normalize(q.d), L.nN);
+        L.mat = (b.rec >= 0) ? s.mesh : b.rec;
+        L.color = v3{0.0f, 0.0f, 0.0f};
+        L.li = 0;
+        L.desc = false;
+        if (L.level < P.max_level) {
+            const v3 ks{s.m.ks[0], s.m.ks[1], s.m.ks[2]};
+            if (s.m.transp == 1.0f) {
+                if (ks.x > 0.0f || ks.y > 0.0f || ks.z > 0.0f) L.desc = true;
+            } else {
+                // Schlick Fresnel with R0 = transparency, Snell with eta = refraction_factor: the reflected
+                // child after the lights, the refracted one (if traced) pushed
+                const v3 l = normalize(q.d);
+                const v3 n = L.nN;
+                const float r = P.refr;
+                const float c = fabsf(dot(l, n));
+                v3 refr = r * l + (r * c - sqrtf(1.0f - r * r * (1.0f - c * c))) * n;
+                refr = normalize(refr);
+                const float R0 = s.m.transp;
+                const float reflC = (float)((double)R0 + (double)(1.0f - R0) * pow((double)(1.0f - c), 5.0));
+                const float refrC = 1.0f - reflC;
+                L.desc = true;
+                L.rc = reflC;
+                if (r * r * (1.0f - c * c) <= 1.0f) {
+                    const v3 fo = L.hp + 0.01f * refr, fw = L.w * refrC;
+                    float4* fp = tree_frame(P, (int)L.nfr);
+                    fp[0] = make_float4(fo.x, fo.y, fo.z, __int_as_float((int)L.level + 1));
+                    fp[1] = make_float4(refr.x, refr.y, refr.z, 0.0f);
+                    fp[2] = make_float4(fw.x, fw.y, fw.z, 0.0f);
+                    L.nfr++;
+                }
+            }
+        }
+    } else {
+        node_done = false;  // a miss: getFinalColor returns black
+    }
+    if (node_done) {
+        const int r = tree_next_light(P, L, q, sdist, sI);
+        if (r == 1) {
+            L.shadow = true;
+            return TA_QUERY;
+        }
+        if (r == 2) return TA_FAN;
+        L.acc = L.acc + L.w * L.color;  // every light done: the node's colour, then its child
+        if (L.desc) {
+            const DMat m = load_mat(S, L.mat);
+            if (m.transp == 1.0f) {
+                const v3 ks{m.ks[0], m.ks[1], m.ks[2]};
+                L.w = (m.shin != 0.0f) ? L.w * ((ks * ks) / (float)P.glossy_n) : L.w * (ks * ks);
+            } else {
+                L.w = L.w * L.rc;
+            }
+            L.level++;
+            q.o = L.hp + 0.01f * L.refl;
+            q.d = L.refl;
+            q.t = FLT_MAX;
+            return TA_QUERY;
+        }
+    }
+    // the subtree is finished: the deepest pending refracted ray (next_branch)
+    if (L.nfr > 0) {
+        L.nfr--;
+        const float4* fp = tree_frame(P, (int)L.nfr);
+        const float4 f0 = fp[0], f1 = fp[1], f2 = fp[2];
+        L.level = (uint32_t)__float_as_int(f0.w);
+        L.w = v3{f2.x, f2.y, f2.z};
+        q.o = v3{f0.x, f0.y, f0.z};
+        q.d = v3{f1.x, f1.y, f1.z};
+        q.t = FLT_MAX;
+        return TA_QUERY;
+    }
+    // camera sample complete
+    if (store_sample(P, L.job, L.sample, L.acc)) {
+        L.sample++;
+        uint32_t rpix;
+        int out_row;
+        job_pixel(P, L.job, rpix, out_row);
+        camera_query(P, L.job, rpix, L.sample, q);
+        L.acc = v3{0.0f, 0.0f, 0.0f};
+        L.w = v3{1.0f, 1.0f, 1.0f};
+        L.level = 0;
+        L.desc = false;
+        return TA_QUERY;
+    }
+    L.job = -1;
+    return TA_DONE;
+}
+
+template <bool COUNT, int V>
+__global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_tree_kernel(KParams, JobSrc) {
+    constexpr bool PF = !(V & RT_V_NOPF);
+    const void* ka = (const void*)__builtin_amdgcn_kernarg_segment_ptr();
+#define RT_FRESH const KParams& P = *(const KParams*)fresh_kernarg(ka); const DevScene& S = P.S
+    __shared__ int stack_lds[RT_STACK8 * RT_WAVE];
+    __shared__ int s_base, s_lim;
+    __shared__ FanTable ft;
+    __shared__ int fan_queue[RT_WAVE];  // lanes waiting for a fan slot, oldest first
+    const int lane_id = threadIdx.x;
+    int* stk = stack_lds + lane_id;
+    if (lane_id < FAN_SLOTS) ft.owner[lane_id] = -1;
+    __syncthreads();
+    int fq_head = 0, fq_tail = 0;  // (wave-uniform)
+    bool fq_in = false;            // this lane is in the fan queue
+    int own_fan = -1;              // fan slot this lane's state machine waits for
+    bool fan_req = false;          // the state machine posted a fan, no free slot yet
+    int ray_fan = -1, ray_s = 0;   // the fan sample this lane's traversal slot traces
+    float qsI = 1.0f, qsdist = 0.0f;  // cansee intensity / remaining distance of the segment in flight
+    TreeLane L;
+    L.job = -1;
+    L.shadow = false;
+    L.nfr = 0;
+    Trav T;
+    Cnt cnt{};
+    int xr = (int)(blockIdx.x & 7), xtried = 0;
+    bool tracing = false, pending = false;
+    for (;;) {
+        unsigned long long tA = COUNT ? (unsigned long long)clock64() : 0ull;
+        RT_FRESH;
+        const JobSrc& J = kernel_jobs(&P);
+        bool start = false, qshadow = false;
+        Query q;
+        // ---- a finished cansee segment (the lane's own, or a fan sample): next segment, or its result ----
+        int vis = 0;
+        if (pending && (ray_fan >= 0 || L.shadow)) {
+            q.o = T.o;
+            q.d = T.d;
+            const int r = S.all_opaque ? (T.found ? 0 : 1) : cansee_step(S, q, T.found, T.best, qsI, qsdist);
+            if (r == 2) {  // past a transparent surface: the segment loop goes on
+                pending = false;
+                start = true;
+                qshadow = true;
+            } else if (ray_fan >= 0) {
+                pending = false;
+                if (r == 1 && ft.plane[ray_fan]) fan_plane_term(P, ft, ray_fan, ray_s);
+                fan_record(ft, ray_fan, ray_s, r == 1, qsI);
+                ray_fan = -1;
+            } else {
+                vis = r;
+            }
+        }
+        __syncthreads();
+        // ---- owners of complete fans resume once their traversal slot is free ----
+        FanResult fan{0ull, nullptr, false, nullptr, 0.0f};
+        if (own_fan >= 0 && !tracing && !start && ft.done[own_fan] == ft.count[own_fan]) {
+            fan.vis = ft.vis[own_fan];
+            fan.inten = S.all_opaque ? nullptr : ft.inten[own_fan];
+            fan.term = ft.term[own_fan];
+            fan.c2max = __uint_as_float(ft.c2max[own_fan]);
+            fan.done = true;
+            ft.owner[own_fan] = -1;
+            own_fan = -1;
+        }
+        if (pending || fan.done) {
+            pending = false;
+            if (COUNT && wave_leader()) cnt.wadv++;
+            if (!fan.done && !L.shadow) {
+                q.o = T.o;
+                q.d = T.d;
+            }
+            const int jb = L.job;
+            const int r = tree_advance<COUNT>(P, L, vis, fan, T.found, T.best, q, qsdist, qsI, cnt);
+            if (r == TA_QUERY) {
+                start = true;
+                qshadow = L.shadow;
+            } else if (r == TA_FAN) {
+                fan_req = true;
+            }
+            if (COUNT && P.job_trace && L.job == -1) P.job_trace[3 * jb + 1] = wall_clock64();
+        }
+        __syncthreads();
+        // ---- fan slots to the oldest posters, then samples to every lane whose traversal slot is free ----
+        {
+            const bool new_req = fan_req && !fq_in;
+            const unsigned long long nr = __ballot(new_req);
+            if (nr) {
+                if (new_req) {
+                    fan_queue[(fq_tail + __popcll(nr & ((1ull << lane_id) - 1ull))) & (RT_WAVE - 1)] = lane_id;
+                    fq_in = true;
+                }
+                fq_tail += __popcll(nr);
+                __syncthreads();
+            }
+            if (fq_head != fq_tail) {
+                uint64_t freeslots = __ballot(lane_id < FAN_SLOTS && ft.owner[lane_id] < 0);
+                while (fq_head != fq_tail && freeslots) {
+                    const int l = fan_queue[fq_head & (RT_WAVE - 1)], f = __ffsll((long long)freeslots) - 1;
+                    ++fq_head;
+                    freeslots &= freeslots - 1ull;
+                    if (lane_id == l) {
+                        const bool plane = (int)L.li >= S.npl + S.nsl;
+                        fq_in = false;
+                        ft.owner[f] = l;
+                        ft.next[f] = 0;
+                        ft.plane[f] = plane ? 1 : 0;
+                        ft.count[f] = plane ? P.plane_k * P.plane_k : 1 + P.sl_m * P.sl_n;
+                        ft.done[f] = 0;
+                        ft.traced[f] = 0;
+                        ft.vis[f] = 0ull;
+                        ft.li[f] = plane ? (int)L.li - S.npl - S.nsl - S.nspot : (int)L.li - S.npl;
+                        ft.hx[f] = L.hp.x;
+                        ft.hy[f] = L.hp.y;
+                        ft.hz[f] = L.hp.z;
+                        ft.rx[f] = L.refl.x;
+                        ft.ry[f] = L.refl.y;
+                        ft.rz[f] = L.refl.z;
+                        ft.c2max[f] = 0u;
+                        own_fan = f;
+                        fan_req = false;
+                    }
+                }
+                __syncthreads();
+            }
+            const bool tfree = !tracing && !start;
+            const unsigned long long fl = __ballot(tfree);
+            uint64_t pend =
+                __ballot(lane_id < FAN_SLOTS && ft.owner[lane_id] >= 0 && ft.next[lane_id] < ft.count[lane_id]);
+            if (fl && pend) {
+                const int nfree = __popcll(fl);
+                const int rank = __popcll(fl & ((1ull << lane_id) - 1ull));
+                int base = 0;
+                while (pend && base < nfree) {
+                    const int f = __ffsll((long long)pend) - 1;
+                    pend &= pend - 1ull;
+                    const int nx = ft.next[f];
+                    const int take = min(ft.count[f] - nx, nfree - base);
+                    if (tfree && rank >= base && rank < base + take) {
+                        ray_fan = f;
+                        ray_s = nx + (rank - base);
+                    }
+                    __syncthreads();
+                    if (lane_id == 0) ft.next[f] = nx + take;
+                    base += take;
+                }
+                __syncthreads();
+            }
+            if (tfree && ray_fan >= 0) {
+                const v3 hp{ft.hx[ray_fan], ft.hy[ray_fan], ft.hz[ray_fan]};
+                qsI = 1.0f;
+                if (fan_sample_query(P, hp, ft.li[ray_fan], ft.plane[ray_fan], ray_s, q, qsdist)) {
+                    start = true;
+                    qshadow = true;
+                } else {  // visible without a query
+                    if (ft.plane[ray_fan]) fan_plane_term(P, ft, ray_fan, ray_s);
+                    fan_record(ft, ray_fan, ray_s, true, 1.0f);
+                    ray_fan = -1;
+                }
+            }
+            __syncthreads();
+        }
+        const unsigned long long tJ = COUNT ? (unsigned long long)clock64() : 0ull;
+        if (COUNT) cnt.cyc_c += tJ - tA;
+        // ---- new pixels for idle lanes (none while the wave's pixels wait on fan_cap fans) ----
+        const bool fan_full = __popcll(__ballot(own_fan >= 0 || fan_req)) >= P.fan_cap;
+        const bool idle = (L.job == -1) && !start && !tracing && !fan_full;
+        const unsigned long long want = __ballot(idle);
+        if (want) {
+            const int nwant = __popcll(want);
+            if (lane_id == __ffsll((long long)want) - 1) {
+                const int lo = xq_lo(J, xr);
+                s_base = lo + atomicAdd(J.xq + 32 * xr, nwant);
+                s_lim = xr == 7 ? J.njobs : xq_lo(J, xr + 1);
+            }
+            __builtin_amdgcn_wave_barrier();
+            __syncthreads();
+            const int base = s_base, lim = s_lim;
+            if (base + nwant >= lim) {  // this group's range is used up: go on to the next
+                xr = (xr + 1) & 7;
+                ++xtried;
+            }
+            if (idle) {
+                const int job_k = base + __popcll(want & ((1ull << lane_id) - 1ull));
+                if (job_k < lim) {
+                    if (COUNT && P.job_trace) P.job_trace[3 * job_k] = wall_clock64();
+                    int out_row;
+                    L.job = job_k;
+                    uint32_t rpix;
+                    if (job_pixel(P, job_k, rpix, out_row)) {
+                        L.sample = 0;
+                        camera_query(P, job_k, rpix, 0, q);
+                        L.acc = v3{0.0f, 0.0f, 0.0f};
+                        L.w = v3{1.0f, 1.0f, 1.0f};
+                        L.level = 0;
+                        L.desc = false;
+                        L.shadow = false;
+                        L.nfr = 0;
+                        qshadow = false;
+                        start = true;
+                    } else {
+                        L.job = -1;  // a padding pixel
+                    }
+                } else {
+                    L.job = xtried < 8 ? -1 : -2;
+                }
+            }
+            __syncthreads();
+        }
+        if (COUNT) cnt.cyc_d += (unsigned long long)clock64() - tJ;
+        // full-wave phases: the traversal state is rebuilt for every lane (a new query or an empty walk)
+        {
+            Trav Tn;
+            if (start) {
+                cnt.rays++;
+                trav_init_q(S, P.use_bvh != 0, q.o, q.d, q.t, qshadow, qsdist, Tn);
+                tracing = true;
+            } else {
+                trav_idle(Tn);
+            }
+            T = Tn;
+        }
+        if (!__any(tracing)) {
+            if (!__any(L.job == -1 || pending || own_fan >= 0 || fan_req)) break;  // every lane exhausted
+            continue;
+        }
+        // ---- one node visit and / or one leaf record per lane and iteration, until no lane traces ----
+        unsigned long long tB = 0ull;
+        if (COUNT) {
+            tB = (unsigned long long)clock64();
+            cnt.cyc_a += tB - tA;
+        }
+        float4 g[8];
+        if (PF && tracing && T.cur != RT_TRAV_NONE) node_fetch(S.nodes, T.cur, g);
+        for (;;) {
+            if (COUNT) {
+                const int ntr = __popcll(__ballot(tracing));
+                if (wave_leader()) cnt.hist[min((ntr - 1) >> 4, 2)]++;
+            }
+            if (tracing) {
+                const bool rec = leaf_pending(T);
+                if (rec) trav_record<COUNT, true>(S, T, cnt);
+                const bool nv = T.cur != RT_TRAV_NONE && (!rec || (P.dual && T.lh == 0u));
+                if (nv) trav_node<COUNT, 8, PF>(S, T, stk, g, cnt);
+            }
+            if (tracing && !leaf_pending(T) && T.cur == RT_TRAV_NONE) {
+                trav_finish(S, T);
+                tracing = false;
+                pending = true;
+            }
+            if (!__any(tracing)) break;
+        }
+        if (COUNT) cnt.cyc_b += (unsigned long long)clock64() - tB;
+    }
+    const KParams& P = kernel_params(ka);
+    flush_counters<COUNT>(P, cnt);
+#undef RT_FRESH
+}
+
 // BoundingVolumeHierarchy::intersect(ray, hitInfo, useBVH) per ray (rt_intersect): the same
 // trace_query8 and surface() as the renderer.
 __global__ __launch_bounds__(64) void intersect_kernel(DevScene S, const rt_ray* rays, int n, int use_bvh,

@@ -105,6 +105,10 @@ struct rt_ctx {
     bool glossy_material = false;  // opaque, ks > 0, shininess != 0 (glossy_ray_count > 1 draws lobes)
     int persistent_blocks[1024] = {0};  // resident 64-lane blocks per (kernel class, variant)
     int opaque_blocks[2] = {0, 0};      // ... of the opaque-scene kernel
+    int tree_blocks[2] = {0, 0};        // ... of the recursion-tree kernel
+    // recursion-tree kernel: the lanes' pending refracted rays (KParams::frames)
+    float* d_frames = nullptr;
+    size_t frames_bytes = 0;
     // lights (re-uploadable: rt_update_lights)
     void* d_lights[4] = {nullptr, nullptr, nullptr, nullptr};
     // developer wave trace (RT_OPT_WAVE_TRACE)
@@ -130,6 +134,7 @@ struct rt_ctx {
     int opt_dual = -1;        // dynamic-fetch steps: record and node visit in one iteration (-1 default, 0 off, 1 on)
     int opt_variant = -1;   // -1: the shipped variant for the render shape (RT_DF_BATCH / _FRAME, RT_WT_DEFAULT)
     int opt_opaque = -1;    // opaque-scene kernel: -1 where eligible (build by render shape), 0 never, 1 / 2 the 4- / 3-wave build
+    int opt_tree = -1;      // recursion-tree kernel: -1 where eligible (build by render shape), 0 never, 1 / 2 the 4- / 3-wave build
     char last_kernel[64] = {0};
     // view batches: the camera table's pinned host staging and the event of its last copy (the buffer
     // is refilled only once that copy has read it)
@@ -145,7 +150,28 @@ struct rt_ctx {
     std::vector<std::unique_ptr<DeviceWorker>> workers;
     hipEvent_t ev_ready = nullptr;  // devices[0]: the caller stream's work before a split render
     hipEvent_t ev_done = nullptr;   // this replica's part of the last split render
+    // the exchange of a split render: a replica with peer access to devices[0] stores its pixels straight
+    // into the caller's images; one without it (no xGMI peer path, RT_OPT_PEER_STORES 0, or images the
+    // library opened from another process) renders band-dense into d_bands on its own device, copies them
+    // into stage[i] on devices[0] (hipMemcpyPeerAsync) and one scatter launch there puts them in place
+    bool peer_ok = true;   // rt_create: peer access to devices[0] is enabled (or the same device)
+    int opt_peer = -1;     // RT_OPT_PEER_STORES: -1 where peer access works, 0 never
+    float* d_bands = nullptr;
+    size_t bands_bytes = 0;
+    std::vector<float*> stage;        // devices[0] (primary context only): replica i's band copy
+    std::vector<size_t> stage_bytes;
 };
+
+// device ranges this library opened from other processes (rt_ipc_open): mapped for the opening device only
+static std::mutex g_ipc_mu;
+static std::vector<std::pair<uintptr_t, size_t>> g_ipc_ranges;
+static bool ipc_mapped(const void* p) {
+    std::lock_guard<std::mutex> lk(g_ipc_mu);
+    const uintptr_t a = (uintptr_t)p;
+    for (const auto& r : g_ipc_ranges)
+        if (a >= r.first && a < r.first + r.second) return true;
+    return false;
+}
 
 // Image::Image + initMipmap (src/image.cpp:37-73,408-452): texel k = rgb[k*channels + 0..2] / 255.0f
 // (the reference strides by the file's channel count over the 3-channel stb buffer; bytes past
@@ -236,6 +262,9 @@ extern "C" int rt_destroy(rt_ctx* c) {
     for (size_t i = 1; i < c->replicas.size(); ++i) rt_destroy(c->replicas[i]);
     c->replicas.clear();
     hipSetDevice(c->device);
+    for (float* p : c->stage)
+        if (p) hipFree(p);
+    if (c->d_bands) hipFree(c->d_bands);
     if (c->ev_ready) hipEventDestroy(c->ev_ready);
     if (c->ev_done) hipEventDestroy(c->ev_done);
     if (c->ev_views) hipEventDestroy(c->ev_views);
@@ -249,6 +278,7 @@ extern "C" int rt_destroy(rt_ctx* c) {
     if (c->ev1) hipEventDestroy(c->ev1);
     if (c->d_wave_trace) hipFree(c->d_wave_trace);
     if (c->d_views) hipFree(c->d_views);
+    if (c->d_frames) hipFree(c->d_frames);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
     return RT_OK;
@@ -631,23 +661,19 @@ extern "C" int rt_create(const rt_scene_desc* desc, const int* devices, int ndev
             rc = rcs[i];
             err = errs[i];
         }
-    // the other devices write their pixels straight into devices[0]'s images: peer access to it
+    // the other devices write their pixels straight into devices[0]'s images where they have peer access
+    // to it; a device without (no peer path, or enabling it fails) renders band-dense and copies (rt_ctx)
     for (int i = 1; i < ndev && rc == RT_OK; ++i) {
         if (devices[i] == devices[0]) continue;
         int can = 0;
         hipSetDevice(devices[i]);
         if (hipDeviceCanAccessPeer(&can, devices[i], devices[0]) != hipSuccess || !can) {
-            rc = RT_ERR_HIP;
-            err = "rt_create: device " + std::to_string(devices[i]) + " has no peer access to device " +
-                  std::to_string(devices[0]);
-            break;
+            reps[i]->peer_ok = false;
+        } else {
+            const hipError_t e = hipDeviceEnablePeerAccess(devices[0], 0);
+            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) reps[i]->peer_ok = false;
         }
-        const hipError_t e = hipDeviceEnablePeerAccess(devices[0], 0);
-        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
-            rc = RT_ERR_HIP;
-            err = std::string("rt_create: hipDeviceEnablePeerAccess: ") + hipGetErrorString(e);
-        }
-        (void)hipGetLastError();  // (an already-enabled peer leaves a sticky status)
+        (void)hipGetLastError();  // (an already-enabled or refused peer leaves a sticky status)
     }
     for (int i = 0; i < ndev && rc == RT_OK; ++i) {
         hipSetDevice(devices[i]);
@@ -666,6 +692,8 @@ extern "C" int rt_create(const rt_scene_desc* desc, const int* devices, int ndev
     rt_ctx* c = reps[0];
     c->devices.assign(devices, devices + ndev);
     c->replicas = reps;
+    c->stage.assign(ndev, nullptr);
+    c->stage_bytes.assign(ndev, 0);
     c->workers = std::move(workers);
     hipSetDevice(devices[0]);
     *out = c;
@@ -679,6 +707,18 @@ extern "C" int rt_ctx_devices(rt_ctx* c, int* out, int n) {
     }
     const int nd = (int)c->devices.size();
     for (int i = 0; i < n && i < nd && out; ++i) out[i] = c->devices[i];
+    return nd;
+}
+
+// 1 per replica that stores its pixels straight into devices[0] (peer access), 0 for one that copies
+extern "C" int rt_ctx_peer_stores(rt_ctx* c, int* out, int n) {
+    if (!c) {
+        set_error("rt_ctx_peer_stores: null ctx");
+        return RT_ERR_INVALID;
+    }
+    const int nd = (int)c->replicas.size();
+    for (int i = 0; i < n && i < nd && out; ++i)
+        out[i] = (i == 0 || (c->replicas[i]->peer_ok && c->replicas[i]->opt_peer != 0)) ? 1 : 0;
     return nd;
 }
 
@@ -831,6 +871,14 @@ static int set_option_one(rt_ctx* c, int option, int value) {
             if (value < -1 || value > 2) break;
             c->opt_opaque = value;
             return RT_OK;
+        case RT_OPT_TREE:
+            if (value < -1 || value > 2) break;
+            c->opt_tree = value;
+            return RT_OK;
+        case RT_OPT_PEER_STORES:
+            if (value < -1 || value > 0) break;
+            c->opt_peer = value;
+            return RT_OK;
         default:
             set_error("rt_ctx_set_option: unknown option");
             return RT_ERR_INVALID;
@@ -902,6 +950,25 @@ static bool opaque_w3(const rt_ctx* c, const KParams& K) {
     return c->opt_opaque == 2 || (c->opt_opaque != 1 && K.n_views <= 1);
 }
 
+// the recursion-tree kernel (rt_megakernel.hip persistent_tree_kernel): 4 / 3 waves per SIMD
+#define RT_TREE_V (RT_V_W4 | RT_V_NOPF)
+#define RT_TREE_V3 (RT_V_W3 | RT_V_NOPF)
+
+// Renders that the recursion-tree kernel draws: pixels of a dynamic-fetch-class render the opaque kernel
+// does not take, without textures or glossy lobes, whose spherical and plane lights fit one fan (<= 64
+// samples; fans on).  RT_OPT_TREE 0 and any RT_OPT_VARIANT choice select the general kernels instead.
+static bool tree_path(const rt_ctx* c, const KParams& K, bool pixels) {
+    if (!pixels || c->opt_tree == 0 || c->opt_variant >= 0 || !c->opt_fan || !use_df(c, K) || opaque_path(c, K, pixels))
+        return false;
+    if (K.S.tex_on || !(K.glossy_n == 1 || !c->glossy_material)) return false;
+    if (K.S.nsl > 0 && 1 + K.sl_m * K.sl_n > 64) return false;
+    if (K.S.nplane > 0 && K.plane_k * K.plane_k > 64) return false;
+    return (long long)K.S.npl + K.S.nsl + K.S.nspot + K.S.nplane < 65536;  // TreeLane::li
+}
+static bool tree_w3(const rt_ctx* c, const KParams& K) {
+    return c->opt_tree == 2 || (c->opt_tree != 1 && K.n_views <= 1);
+}
+
 // by render shape: view batches and sample-fan renders run the lean 4-wave variant (C4 single frame
 // with fans: 27.1 vs 30.3 ms), other single frames the 2-wave variant with the drain lane groups
 static int variant_of(const rt_ctx* c, bool df, const KParams& K) {
@@ -937,6 +1004,14 @@ static int launch_persistent(int grid, hipStream_t st, const KParams& K, const J
         else hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V>), dim3(grid), dim3(64), 0, st, K, J);
         std::snprintf(c->last_kernel, sizeof(c->last_kernel), "rt::persistent_opaque_kernel<%s, %d>",
                       COUNT ? "true" : "false", w3 ? RT_OPAQUE_V3 : RT_OPAQUE_V);
+        return RT_OK;
+    }
+    if (tree_path(c, K, J.mode == 0)) {
+        const bool w3 = tree_w3(c, K);
+        if (w3) hipLaunchKernelGGL((persistent_tree_kernel<COUNT, RT_TREE_V3>), dim3(grid), dim3(64), 0, st, K, J);
+        else hipLaunchKernelGGL((persistent_tree_kernel<COUNT, RT_TREE_V>), dim3(grid), dim3(64), 0, st, K, J);
+        std::snprintf(c->last_kernel, sizeof(c->last_kernel), "rt::persistent_tree_kernel<%s, %d>",
+                      COUNT ? "true" : "false", w3 ? RT_TREE_V3 : RT_TREE_V);
         return RT_OK;
     }
     const bool df = use_df(c, K);
@@ -980,6 +1055,18 @@ static int persistent_grid(rt_ctx* c, const KParams& K, bool pixels) {
         if (e != hipSuccess || per_cu <= 0) per_cu = 8;
         c->opaque_blocks[key] = std::max(1, cus) * per_cu;
         return c->opaque_blocks[key];
+    }
+    if (tree_path(c, K, pixels)) {
+        const int key = tree_w3(c, K) ? 1 : 0;
+        if (c->tree_blocks[key] > 0) return c->tree_blocks[key];
+        int cus = 0, per_cu = 0;
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
+        const hipError_t e =
+            key ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_tree_kernel<false, RT_TREE_V3>, 64, 0)
+                : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_tree_kernel<false, RT_TREE_V>, 64, 0);
+        if (e != hipSuccess || per_cu <= 0) per_cu = 8;
+        c->tree_blocks[key] = std::max(1, cus) * per_cu;
+        return c->tree_blocks[key];
     }
     const bool df = use_df(c, K);
     const int v = variant_of(c, df, K);
@@ -1169,6 +1256,14 @@ static int launch_render(rt_ctx* c, KParams& K, hipStream_t st, int count_mode, 
         J.counter = reinterpret_cast<int*>(c->d_stats + 7);
         J.xq = use_df(c, K) ? reinterpret_cast<int*>(c->d_stats + 16) : nullptr;
         const int grid = (int)std::min<long long>(blocks * J.n_views, persistent_grid(c, K, true));
+        if (tree_path(c, K, true)) {
+            // the tree kernel's frame stacks: max_level frames of 48 B per resident lane
+            const size_t slots = (size_t)grid * 64;
+            const int rc = ensure(c, &c->d_frames, &c->frames_bytes, slots * std::max(1, K.max_level) * 48);
+            if (rc != RT_OK) return rc;
+            K.frames = reinterpret_cast<float4*>(c->d_frames);
+            K.frame_slots = (int)slots;
+        }
         if (c->opt_wave_trace) {
             const int rc = ensure(c, &c->d_wave_trace, &c->wave_trace_bytes,
                                   (size_t)grid * 8 * 8 + (size_t)J.njobs * 3 * 8);
@@ -1329,6 +1424,39 @@ static int launch_image(rt_ctx* c, const rt_camera* cams, int n_views, const rt_
     return launch_render(c, K, st, g_count_mode, stats);
 }
 
+// One replica's part of a split render without peer stores: the bands b % band_count == band_rank of every
+// view rendered band-dense into the replica's own d_bands ([view][local band][row][W][3]); returns the
+// buffer's size in *bytes.
+static int launch_bands(rt_ctx* c, const rt_camera* cams, int n_views, const rt_params* p, int W, int H, int band_rows,
+                        int band_rank, int band_count, hipStream_t st, size_t* bytes, rt_stats* stats) {
+    HIP_TRY(hipSetDevice(c->device));
+    KParams K;
+    int rc = fill_params(c, cams, p, W, H, K);
+    if (rc != RT_OK) return rc;
+    const int nbands = (H + band_rows - 1) / band_rows;
+    const int max_local = (nbands + band_count - 1) / band_count;
+    K.band_rows = band_rows;
+    K.band_rank = band_rank;
+    K.band_count = band_count;
+    K.n_local_bands = nbands > band_rank ? (nbands - band_rank + band_count - 1) / band_count : 0;
+    const long long view_jobs = (long long)((W + 7) / 8) * ((band_rows + 7) / 8) * K.n_local_bands * 64;
+    if (view_jobs * n_views > 0x7FFFFFFFll) {
+        set_error("split render: batch too large (job index overflows int)");
+        return RT_ERR_INVALID;
+    }
+    *bytes = (size_t)n_views * max_local * band_rows * W * 3 * sizeof(float);
+    rc = ensure(c, &c->d_bands, &c->bands_bytes, std::max<size_t>(*bytes, 4));
+    if (rc != RT_OK) return rc;
+    K.out = c->d_bands;
+    K.n_views = n_views;
+    K.view_rows = max_local * band_rows;
+    if (n_views > 1) {
+        rc = upload_views(c, cams, n_views, st, K);
+        if (rc != RT_OK) return rc;
+    }
+    return launch_render(c, K, st, g_count_mode, stats);
+}
+
 static void add_stats(rt_stats& a, const rt_stats& b) {
     a.rays += b.rays;
     a.node_visits += b.node_visits;
@@ -1355,14 +1483,39 @@ static int render_split(rt_ctx* c, const rt_camera* cams, int n_views, const rt_
     std::vector<int> rcs(n, RT_OK);
     std::vector<std::string> errs(n);
     const int count = band_count * n;
+    // peer stores, or band-dense + copy: images opened from another process are mapped for devices[0] only
+    const bool foreign = ipc_mapped(d_images);
+    std::vector<char> copy(n, 0);
+    for (int i = 1; i < n; ++i) {
+        const rt_ctx* r = c->replicas[i];
+        copy[i] = (foreign && r->device != c->device) || !r->peer_ok || r->opt_peer == 0;
+    }
+    // the staging buffers on devices[0] (the host thread's device) before the workers copy into them
+    const int nbands = (H + band_rows - 1) / band_rows;
+    const size_t stage_need = (size_t)n_views * ((nbands + count - 1) / count) * band_rows * W * 3 * sizeof(float);
+    for (int i = 1; i < n; ++i)
+        if (copy[i]) {
+            const int rc = ensure(c, &c->stage[i], &c->stage_bytes[i], std::max<size_t>(stage_need, 4));
+            if (rc != RT_OK) return rc;
+        }
     for (int i = 1; i < n; ++i) {
         c->workers[i]->post([&, i] {
             rt_ctx* r = c->replicas[i];
             rcs[i] = hipSetDevice(r->device) == hipSuccess && hipStreamWaitEvent(r->stream, c->ev_ready, 0) == hipSuccess
                          ? RT_OK : RT_ERR_HIP;
-            if (rcs[i] == RT_OK)
+            if (rcs[i] == RT_OK && !copy[i]) {
                 rcs[i] = launch_image(r, cams, n_views, p, W, H, band_rows, band_rank + band_count * i, count, d_images,
                                       r->stream, stats ? &rs[i] : nullptr);
+            } else if (rcs[i] == RT_OK) {
+                size_t bytes = 0;
+                rcs[i] = launch_bands(r, cams, n_views, p, W, H, band_rows, band_rank + band_count * i, count, r->stream,
+                                      &bytes, stats ? &rs[i] : nullptr);
+                if (rcs[i] == RT_OK && bytes > 0 &&
+                    hipMemcpyPeerAsync(c->stage[i], c->device, r->d_bands, r->device, bytes, r->stream) != hipSuccess) {
+                    set_error("split render: hipMemcpyPeerAsync of the band copy failed");
+                    rcs[i] = RT_ERR_HIP;
+                }
+            }
             if (rcs[i] == RT_OK && hipEventRecord(r->ev_done, r->stream) != hipSuccess) rcs[i] = RT_ERR_HIP;
             if (rcs[i] != RT_OK) errs[i] = last_error_text();
         });
@@ -1372,7 +1525,19 @@ static int render_split(rt_ctx* c, const rt_camera* cams, int n_views, const rt_
     for (int i = 1; i < n; ++i) c->workers[i]->wait();
     HIP_TRY(hipSetDevice(c->device));
     for (int i = 1; i < n; ++i)
-        if (rcs[i] == RT_OK) HIP_TRY(hipStreamWaitEvent(st, c->replicas[i]->ev_done, 0));
+        if (rcs[i] == RT_OK) {
+            HIP_TRY(hipStreamWaitEvent(st, c->replicas[i]->ev_done, 0));
+            if (copy[i]) {
+                // the replica's bands from the staging copy to their setPixel places (on devices[0])
+                const int rank = band_rank + band_count * i, max_local = (nbands + count - 1) / count;
+                const size_t total = (size_t)n_views * max_local * band_rows * W;
+                if (total > 0) {
+                    hipLaunchKernelGGL(scatter_bands_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, W,
+                                       H, band_rows, rank, count, max_local, n_views, c->stage[i], d_images);
+                    HIP_TRY(hipGetLastError());
+                }
+            }
+        }
     for (int i = 0; i < n; ++i)
         if (rcs[i] != RT_OK) {
             set_error(errs[i].empty() ? "split render failed on device " + std::to_string(c->devices[i]) : errs[i]);
@@ -1675,11 +1840,30 @@ extern "C" int rt_ipc_open(int device, const uint8_t handle[RT_IPC_HANDLE_BYTES]
     hipIpcMemHandle_t h;
     std::memcpy(&h, handle, RT_IPC_HANDLE_BYTES);
     HIP_TRY(hipIpcOpenMemHandle(d_ptr, h, hipIpcMemLazyEnablePeerAccess));
+    // remembered: a multi-device context's other replicas cannot store into this mapping (render_split)
+    void* base = nullptr;
+    size_t size = 0;
+    if (hipMemGetAddressRange(&base, &size, *d_ptr) != hipSuccess || !base) {
+        base = *d_ptr;
+        size = 1;
+    }
+    (void)hipGetLastError();
+    std::lock_guard<std::mutex> lk(g_ipc_mu);
+    g_ipc_ranges.emplace_back((uintptr_t)base, size);
     return RT_OK;
 }
 
 extern "C" int rt_ipc_close(void* d_ptr) {
     if (!d_ptr) return RT_OK;
+    {
+        std::lock_guard<std::mutex> lk(g_ipc_mu);
+        for (size_t i = 0; i < g_ipc_ranges.size(); ++i)
+            if ((uintptr_t)d_ptr >= g_ipc_ranges[i].first &&
+                (uintptr_t)d_ptr < g_ipc_ranges[i].first + g_ipc_ranges[i].second) {
+                g_ipc_ranges.erase(g_ipc_ranges.begin() + i);
+                break;
+            }
+    }
     HIP_TRY(hipIpcCloseMemHandle(d_ptr));
     return RT_OK;
 }

@@ -134,7 +134,7 @@ EXPORTS = [
     "rt_postprocess_device", "rt_bitmap_device", "rt_postprocess", "rt_bitmap", "rt_encode_bmp", "rt_write_bmp",
     "rt_philox4x32_10", "rt_debug_wave_trace", "rt_debug_job_trace", "rt_debug_create_ms", "rt_set_build_mode", "rt_debug_build_info", "rt_debug_records", "rt_decode_png", "rt_ctx_set_option", "rt_texture_sample",
     "rt_update_lights", "rt_update_materials", "rt_unpermute_views_device", "rt_scene_mesh_count", "rt_scene_mesh_get",
-    "rt_ctx_devices", "rt_render_views_image_device", "rt_ipc_alloc", "rt_ipc_open", "rt_ipc_close", "rt_device_free",
+    "rt_ctx_devices", "rt_ctx_peer_stores", "rt_render_views_image_device", "rt_ipc_alloc", "rt_ipc_open", "rt_ipc_close", "rt_device_free",
     "rt_device_synchronize", "rt_memcpy_dtoh",
 ]
 IPC_HANDLE_BYTES = 64
@@ -154,6 +154,8 @@ OPT_KERNEL, OPT_COOP, OPT_COOP_MAX, OPT_REFILL, OPT_WAVE_TRACE, OPT_VARIANT, OPT
 OPT_DUAL_STEP = 10
 OPT_CENTRE_FIRST = 12  # job order: upper-half XCD tile ranges walked bottom-up (-1 by shape, 0 off, 1 on)
 OPT_OPAQUE = 11  # opaque-scene kernel: -1 where eligible (default), 0 the general kernels, 1 / 2 the 4- / 3-wave build
+OPT_PEER_STORES = 14  # split renders: -1 peer stores where peer access works (default), 0 band-dense + copy always
+OPT_TREE = 13  # recursion-tree kernel (C4 / C5 class): -1 where eligible (default), 0 the general kernels, 1 / 2 the 4- / 3-wave build
 KERNEL_AUTO, KERNEL_WHOLE_TRAVERSAL, KERNEL_DYNAMIC_FETCH = 0, 1, 2
 # compiled kernel variants (rt_megakernel.hip RT_V_*, rt_runtime.hip RT_DF_* / RT_WT_*)
 V_CALL, V_NOPF, V_NOCOOP, V_W4 = 1, 2, 4, 16
@@ -255,6 +257,7 @@ def lib():
                                          P(rt_camera)], C.c_int),
             "rt_create": ([P(rt_scene_desc), P(C.c_int), C.c_int, P(vp)], C.c_int),
             "rt_ctx_devices": ([vp, P(C.c_int), C.c_int], C.c_int),
+            "rt_ctx_peer_stores": ([vp, P(C.c_int), C.c_int], C.c_int),
             "rt_render_views_image_device": ([vp, P(rt_camera), C.c_int, P(rt_params), C.c_int, C.c_int, C.c_int,
                                               C.c_int, C.c_int, vp, vp, P(rt_stats)], C.c_int),
             "rt_ipc_alloc": ([C.c_int, C.c_size_t, P(vp), P(C.c_uint8)], C.c_int),
@@ -499,6 +502,12 @@ class Context:
             self.h = C.c_void_p()
 
     def __del__(self):
+        # nothing during interpreter shutdown: HIP's own teardown may already have run, and destroying
+        # device resources after it can hang or fault the process -- close() contexts explicitly
+        import sys as _sys
+
+        if getattr(_sys, "is_finalizing", lambda: False)() or not callable(lib):
+            return
         self.close()
 
     def create_ms(self):
@@ -506,6 +515,15 @@ class Context:
         out = np.zeros(8, np.float64)
         check(lib().rt_debug_create_ms(self.h, out.ctypes.data_as(C.POINTER(C.c_double)), 8))
         return out[:7]
+
+    def peer_stores(self):
+        """rt_ctx_peer_stores: per replica, True if it stores pixels straight into devices[0] (peer access),
+        False if it renders band-dense and copies."""
+        out = (C.c_int * 64)()
+        n = lib().rt_ctx_peer_stores(self.h, out, 64)
+        if n < 0:
+            check(n, "rt_ctx_peer_stores")
+        return [bool(out[i]) for i in range(n)]
 
     def build_info(self):
         """rt_debug_build_info: built on the GPU?, BVH2 nodes, BVH2 depth, BVH8 nodes."""

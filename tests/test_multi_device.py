@@ -64,8 +64,16 @@ def test_replicas_bit_identical(R, scenes, cfg, uv, W, H):
         ctx = R.Context(scene, devices=devs)
         try:
             assert ctx.devices == devs
+            assert ctx.peer_stores() == [True] * len(devs)
             img, s = ctx.render(cam, prm, W, H)
             assert img.tobytes() == ref.tobytes(), devs
+            assert s.rays == st.rays, devs
+            # the exchange of devices without peer access: band-dense renders copied to devices[0] and
+            # scattered into place there (RT_OPT_PEER_STORES 0 forces it for every extra replica)
+            ctx.set_option(R.OPT_PEER_STORES, 0)
+            assert ctx.peer_stores() == [True] + [False] * (len(devs) - 1)
+            img, s = ctx.render(cam, prm, W, H)
+            assert img.tobytes() == ref.tobytes(), (devs, "copy exchange")
             assert s.rays == st.rays, devs
         finally:
             ctx.close()
@@ -82,17 +90,19 @@ def test_replicas_view_batch_and_rank_split(R, scenes, cfg, uv, W, H):
     ref, st = ctx1.render_views(cams, prm, W, H)
     ctx = R.Context(scene, devices=[0, 0])
     try:
-        got, s = ctx.render_views(cams, prm, W, H)
-        assert got.tobytes() == ref.tobytes()
-        assert s.rays == st.rays
-        imgs = torch.full((3 * W * H * 3,), -1.0, dtype=torch.float32, device="cuda")
-        rays = 0
-        for rank in range(2):
-            rays += ctx.render_views_image_device(cams, prm, W, H, imgs.data_ptr(), None, band_rank=rank,
-                                                  band_count=2).rays
-        torch.cuda.synchronize()
-        assert imgs.cpu().numpy().reshape(3, -1).tobytes() == ref.tobytes()
-        assert rays == st.rays
+        for peer in (-1, 0):  # peer stores, then the band-copy exchange
+            ctx.set_option(R.OPT_PEER_STORES, peer)
+            got, s = ctx.render_views(cams, prm, W, H)
+            assert got.tobytes() == ref.tobytes(), peer
+            assert s.rays == st.rays
+            imgs = torch.full((3 * W * H * 3,), -1.0, dtype=torch.float32, device="cuda")
+            rays = 0
+            for rank in range(2):
+                rays += ctx.render_views_image_device(cams, prm, W, H, imgs.data_ptr(), None, band_rank=rank,
+                                                      band_count=2).rays
+            torch.cuda.synchronize()
+            assert imgs.cpu().numpy().reshape(3, -1).tobytes() == ref.tobytes(), peer
+            assert rays == st.rays
     finally:
         ctx.close()
 
@@ -133,20 +143,31 @@ def test_create_rejects_bad_device_lists(R, scenes):
         R.Context(scene, devices=[])
 
 
-def test_bench_ipc_exchange_two_processes(R, tmp_path):
-    """bench.py's N > 1 path with the IPC exchange, two ranks (gloo control plane, both on GPU 0):
-    rank 1's kernels store into rank 0's images; the result equals one process rendering the views."""
+@pytest.mark.parametrize("mode", ["ipc", "ipc_fail_rank0", "none"])
+def test_bench_ipc_exchange_two_processes(R, tmp_path, mode):
+    """bench.py's N > 1 path, two ranks (gloo control plane, both on GPU 0).  ipc: rank 1's kernels store
+    into rank 0's images; the result equals one process rendering the views.  ipc_fail_rank0: rank 0's
+    IPC export fails (test hook) -- every rank still meets in the same collectives and the run falls back
+    to the gather scheme with the same images.  none: the no-exchange control leg runs (each rank's bands
+    into its own images)."""
     W, H, F = 160, 90, 3
     out = str(tmp_path / "imgs.npy")
     env = dict(os.environ, BENCH_DIST_BACKEND="gloo", PYTHONUNBUFFERED="1")
+    if mode == "ipc_fail_rank0":
+        env["BENCH_IPC_FAIL_RANK0"] = "1"
+    port = {"ipc": 29511, "ipc_fail_rank0": 29512, "none": 29513}[mode]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
-           "127.0.0.1", "--master-port", str(29511), os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "1",
+           "127.0.0.1", "--master-port", str(port), os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "1",
            "--warmup", "0", "--views", str(F), "--config", "C3", "--dragon-uv", "200x80", "--resolution",
-           f"{W}x{H}", "--no-cpu-baseline", "--dump-images", out]
+           f"{W}x{H}", "--no-cpu-baseline", "--dump-images", out,
+           "--exchange", "none" if mode == "none" else "ipc"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=REPO)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
-    assert "IPC-mapped" in line, line
+    if mode == "none":
+        assert "NO exchange" in line, line
+        return
+    assert ("IPC-mapped" if mode == "ipc" else "all-gather") in line, line
     got = np.load(out)
     scene, prm, _, _, _ = R.build_config("C3", dragon_uv=(200, 80))
     ctx = R.Context(scene)

@@ -7,7 +7,7 @@ import contextlib
 def defaults(R):
     return {R.OPT_KERNEL: R.KERNEL_AUTO, R.OPT_VARIANT: -1, R.OPT_COOP: -1, R.OPT_COOP_MAX: 0, R.OPT_REFILL: 0,
             R.OPT_FAN: 1, R.OPT_INTERLEAVE: -1, R.OPT_FAN_CAP: 0, R.OPT_DUAL_STEP: -1, R.OPT_OPAQUE: -1,
-            R.OPT_CENTRE_FIRST: -1}
+            R.OPT_CENTRE_FIRST: -1, R.OPT_TREE: -1}
 
 
 def kernel_classes(R):
@@ -38,6 +38,9 @@ def all_variants(R):
         {R.OPT_KERNEL: df, R.OPT_OPAQUE: 2},                    # ... its 3-wave (single-frame) build
         {R.OPT_KERNEL: df, R.OPT_REFILL: 32},                   # ... and a half-wave refill
         {R.OPT_KERNEL: df, R.OPT_COOP: 1},                      # ... drain lane groups in the drain only
+        {R.OPT_KERNEL: df, R.OPT_TREE: 0},                      # general kernels where the tree kernel is eligible
+        {R.OPT_KERNEL: df, R.OPT_TREE: 1},                      # the tree kernel's 4-wave build
+        {R.OPT_KERNEL: df, R.OPT_TREE: 2},                      # ... its 3-wave build
     ]
     return out
 
