@@ -409,6 +409,11 @@ int rt_debug_build_info(rt_ctx* ctx, int* out, int n);
 /* Triangle records [first, first + count) as the kernels read them: 16 floats each (v0, n.x, v1, n.y,
  * v2, n.z, D, then scene index / reference-BVH key / reference leaf as int bits). */
 int rt_debug_records(rt_ctx* ctx, float* out, int first, int count);
+/* The reference depth-4 BVH the kernels use (constructBVH, src/bounding_volume_hierarchy.cpp:108-217),
+ * read back from the device: node boxes [nref][6] (lower, upper; BFS creation order), per node its leaf id
+ * or -1, per object (triangles in scene order, then spheres) its leaf id and depth-first visit key (a
+ * leaf's stored object list = its objects by key).  Null outputs are skipped; returns nref. */
+int rt_debug_ref_bvh(rt_ctx* ctx, float* boxes, int* node_leaf, int* obj_leaf, int* obj_key);
 
 /* Introspection for tests / roofline accounting. */
 int rt_ctx_info(rt_ctx* ctx, int* num_nodes, int* num_tri_records, int* ref_bvh_nodes,

@@ -36,6 +36,7 @@ def lib():
         L.oracle_destroy.argtypes = [vp]
         L.oracle_bvh_info.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.oracle_bvh_nodes.argtypes = [vp, F3, C.POINTER(C.c_int), C.c_int]
+        L.oracle_bvh_children.argtypes = [vp, C.c_int, C.POINTER(C.c_int), C.c_int]
         L.oracle_intersect.argtypes = [vp, vp, C.c_int, C.c_int, vp]
         L.oracle_shade.argtypes = [vp, vp, C.c_int, vp, F3, C.POINTER(C.c_uint64)]
         L.oracle_camera.argtypes = [F3, F3, C.c_float, C.c_float, C.c_float, F3]
@@ -68,6 +69,10 @@ class Oracle:
         self.h = lib().oracle_create(C.addressof(d))
 
     def __del__(self):
+        import sys as _sys
+
+        if getattr(_sys, "is_finalizing", lambda: False)() or not callable(lib):
+            return  # interpreter shutdown: the module's globals may be gone
         if getattr(self, "h", None):
             lib().oracle_destroy(self.h)
             self.h = None
@@ -79,6 +84,14 @@ class Oracle:
         leaf = np.zeros(n.value, np.int32)
         lib().oracle_bvh_nodes(self.h, _fp(boxes), leaf.ctypes.data_as(C.POINTER(C.c_int)), n.value)
         return boxes.reshape(-1, 6), leaf
+
+    def bvh_children(self, node):
+        """constructBVH's stored children of `node`: node indices (inner) or, for a leaf, its objects in
+        stored order (triangle scene index; spheres as num_triangles + sphere index)."""
+        n = lib().oracle_bvh_children(self.h, int(node), None, 0)
+        out = np.zeros(max(n, 1), np.int32)
+        lib().oracle_bvh_children(self.h, int(node), out.ctypes.data_as(C.POINTER(C.c_int)), n)
+        return out[:n]
 
     def intersect(self, rays, use_bvh, hit_dtype):
         rays = np.ascontiguousarray(rays)

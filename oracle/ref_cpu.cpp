@@ -936,6 +936,18 @@ int oracle_bvh_nodes(oracle_scene* o, float* boxes, int* is_leaf, int cap) {
     return n;
 }
 
+// node `node`'s children as constructBVH stored them (src/bounding_volume_hierarchy.cpp:108-217): node
+// indices for an inner node; for a leaf its objects in stored order, triangles as their scene index and
+// spheres as num_triangles + sphere index.  Returns the count (copies at most cap).
+int oracle_bvh_children(oracle_scene* o, int node, int* out, int cap) {
+    if (node < 0 || node >= (int)o->sc.nodes.size()) return -1;
+    const Node& nd = o->sc.nodes[node];
+    const int ntri = (int)o->sc.tris.size();
+    const int n = (int)nd.kids.size();
+    for (int i = 0; i < n && i < cap; ++i) out[i] = (nd.leaf && !nd.tri[i]) ? ntri + nd.kids[i] : nd.kids[i];
+    return n;
+}
+
 int oracle_intersect(oracle_scene* o, const rt_ray* rays, int n, int use_bvh, rt_hit* out) {
     for (int i = 0; i < n; ++i) {
         Ray r;

@@ -749,6 +749,56 @@ extern "C" int rt_debug_records(rt_ctx* c, float* out, int first, int count) {
     return RT_OK;
 }
 
+// The reference depth-4 BVH (src/bounding_volume_hierarchy.cpp:108-217) as the context's kernels use it,
+// read back from the device: node boxes [nref][6] (lo, hi; BFS creation order), per node its leaf id or -1,
+// and per object (triangles in scene order, then spheres) its leaf id and depth-first visit key -- a leaf's
+// stored object list is its objects ordered by key.  Any output may be null; returns nref.
+extern "C" int rt_debug_ref_bvh(rt_ctx* c, float* boxes, int* node_leaf, int* obj_leaf, int* obj_key) {
+    if (!c) {
+        set_error("rt_debug_ref_bvh: null ctx");
+        return RT_ERR_INVALID;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    const int nref = c->S.nref;
+    std::vector<DRefNode> refn(nref);
+    std::vector<int> paths(32 * 8);
+    if (nref > 0) HIP_TRY(hipMemcpy(refn.data(), c->S.refn, nref * sizeof(DRefNode), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(paths.data(), c->S.leaf_path, paths.size() * sizeof(int), hipMemcpyDeviceToHost));
+    for (int i = 0; i < nref; ++i) {
+        if (boxes)
+            for (int k = 0; k < 3; ++k) {
+                boxes[i * 6 + k] = refn[i].lo[k];
+                boxes[i * 6 + 3 + k] = refn[i].hi[k];
+            }
+        if (node_leaf) node_leaf[i] = -1;
+    }
+    if (node_leaf)
+        for (int l = 0; l < 32; ++l) {
+            const int cnt = paths[l * 8];
+            if (cnt > 0 && cnt < 8 && paths[l * 8 + cnt] >= 0 && paths[l * 8 + cnt] < nref) node_leaf[paths[l * 8 + cnt]] = l;
+        }
+    if (obj_leaf || obj_key) {
+        std::vector<float> rec((size_t)c->nrec * 16);
+        if (c->nrec > 0) HIP_TRY(hipMemcpy(rec.data(), c->S.tri, rec.size() * sizeof(float), hipMemcpyDeviceToHost));
+        for (int r = 0; r < c->nrec; ++r) {
+            int sidx, key, leaf;
+            std::memcpy(&sidx, &rec[(size_t)r * 16 + 13], 4);
+            std::memcpy(&key, &rec[(size_t)r * 16 + 14], 4);
+            std::memcpy(&leaf, &rec[(size_t)r * 16 + 15], 4);
+            if (sidx < 0 || sidx >= c->ntri) continue;
+            if (obj_leaf) obj_leaf[sidx] = leaf;
+            if (obj_key) obj_key[sidx] = key;
+        }
+        std::vector<DSph> sph(c->S.nsph);
+        if (!sph.empty()) HIP_TRY(hipMemcpy(sph.data(), c->S.sph, sph.size() * sizeof(DSph), hipMemcpyDeviceToHost));
+        for (int s2 = 0; s2 < (int)sph.size(); ++s2) {
+            if (obj_leaf) obj_leaf[c->ntri + s2] = sph[s2].leaf;
+            if (obj_key) obj_key[c->ntri + s2] = sph[s2].key_bvh;
+        }
+    }
+    return nref;
+}
+
 // rt_create's phase clock (cumulative ms: device, reference BVH, BVH2/BVH8, records, materials and
 // textures, uploads, total)
 extern "C" int rt_debug_create_ms(rt_ctx* c, double* out, int n) {

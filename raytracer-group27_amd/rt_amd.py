@@ -132,7 +132,7 @@ EXPORTS = [
     "rt_destroy", "rt_render", "rt_render_device", "rt_render_views_device", "rt_render_views", "rt_unpermute_bands_device", "rt_intersect", "rt_shade",
     "rt_set_counting", "rt_debug_counters", "rt_ctx_info", "rt_selftest_math",
     "rt_postprocess_device", "rt_bitmap_device", "rt_postprocess", "rt_bitmap", "rt_encode_bmp", "rt_write_bmp",
-    "rt_philox4x32_10", "rt_debug_wave_trace", "rt_debug_job_trace", "rt_debug_create_ms", "rt_set_build_mode", "rt_debug_build_info", "rt_debug_records", "rt_decode_png", "rt_ctx_set_option", "rt_texture_sample",
+    "rt_philox4x32_10", "rt_debug_wave_trace", "rt_debug_job_trace", "rt_debug_create_ms", "rt_set_build_mode", "rt_debug_build_info", "rt_debug_records", "rt_debug_ref_bvh", "rt_decode_png", "rt_ctx_set_option", "rt_texture_sample",
     "rt_update_lights", "rt_update_materials", "rt_unpermute_views_device", "rt_scene_mesh_count", "rt_scene_mesh_get",
     "rt_ctx_devices", "rt_ctx_peer_stores", "rt_render_views_image_device", "rt_ipc_alloc", "rt_ipc_open", "rt_ipc_close", "rt_device_free",
     "rt_device_synchronize", "rt_memcpy_dtoh",
@@ -299,6 +299,7 @@ def lib():
             "rt_set_build_mode": ([C.c_int], C.c_int),
             "rt_debug_build_info": ([vp, P(C.c_int), C.c_int], C.c_int),
             "rt_debug_records": ([vp, P(C.c_float), C.c_int, C.c_int], C.c_int),
+            "rt_debug_ref_bvh": ([vp, P(C.c_float), P(C.c_int), P(C.c_int), P(C.c_int)], C.c_int),
             "rt_ctx_set_option": ([vp, C.c_int, C.c_int], C.c_int),
             "rt_texture_sample": ([vp, C.c_int, C.c_int, P(C.c_float), P(rt_params), P(C.c_float)], C.c_int),
             "rt_update_lights": ([vp, P(rt_scene_desc)], C.c_int),
@@ -524,6 +525,33 @@ class Context:
         if n < 0:
             check(n, "rt_ctx_peer_stores")
         return [bool(out[i]) for i in range(n)]
+
+    def ref_bvh(self):
+        """rt_debug_ref_bvh: (node boxes [n, 6], per node its leaf id or -1, per node its stored children: node
+        indices for inner nodes -- BFS order, two per inner node -- and for leaves the objects in stored
+        order, triangles as scene index, spheres as num_triangles + sphere index)."""
+        nref = lib().rt_debug_ref_bvh(self.h, None, None, None, None)
+        if nref < 0:
+            check(nref, "rt_debug_ref_bvh")
+        d = self.scene.desc()
+        nobj = d.num_triangles + d.num_spheres
+        boxes = np.zeros((max(nref, 1), 6), np.float32)
+        node_leaf = np.zeros(max(nref, 1), np.int32)
+        obj_leaf = np.zeros(max(nobj, 1), np.int32)
+        obj_key = np.zeros(max(nobj, 1), np.int32)
+        ip = lambda a: a.ctypes.data_as(C.POINTER(C.c_int))  # noqa: E731
+        check(lib().rt_debug_ref_bvh(self.h, boxes.ctypes.data_as(C.POINTER(C.c_float)), ip(node_leaf), ip(obj_leaf),
+                                     ip(obj_key)), "rt_debug_ref_bvh")
+        boxes, node_leaf, obj_leaf, obj_key = boxes[:nref], node_leaf[:nref], obj_leaf[:nobj], obj_key[:nobj]
+        children, nxt = [], 1
+        for i in range(nref):
+            if node_leaf[i] >= 0:
+                objs = np.nonzero(obj_leaf == node_leaf[i])[0]
+                children.append(objs[np.argsort(obj_key[objs], kind="stable")].astype(np.int32))
+            else:  # BFS: the inner nodes' children were created in order, two each
+                children.append(np.array([nxt, nxt + 1], np.int32))
+                nxt += 2
+        return boxes, node_leaf, children
 
     def build_info(self):
         """rt_debug_build_info: built on the GPU?, BVH2 nodes, BVH2 depth, BVH8 nodes."""

@@ -72,3 +72,26 @@ def test_gpu_build_is_default_for_large_scenes_and_deterministic():
     finally:
         a.close()
         b.close()
+
+
+@pytest.mark.parametrize("cfg", ["C1", "C2", "C5"])
+def test_builders_reproduce_reference_bvh_dump(cfg, golden_dir):
+    """The reference depth-4 BVH as both builders leave it on the device (host bvh_build.cpp, GPU
+    rt_build.hip) against the oracle's dump in tests/golden/ref_bvh.npz (constructBVH,
+    src/bounding_volume_hierarchy.cpp:108-217): node boxes bit for bit, the same leaves, and each leaf's
+    objects in the reference's stored order (the tie-break keys)."""
+    z = np.load(f"{golden_dir}/ref_bvh.npz")
+    off, ch = z[f"{cfg}__offsets"], z[f"{cfg}__children"]
+    kids = [ch[off[i]:off[i + 1]] for i in range(len(off) - 1)]
+    boxes, leaf = z[f"{cfg}__boxes"], z[f"{cfg}__is_leaf"]
+    s, _, _, _, _ = R.build_config(cfg)
+    for mode in (R.BUILD_HOST, R.BUILD_GPU):
+        ctx = _ctx(s, mode)
+        try:
+            b, node_leaf, got = ctx.ref_bvh()
+            assert b.tobytes() == boxes.tobytes(), mode
+            assert np.array_equal(node_leaf >= 0, leaf.astype(bool)), mode
+            for i in range(len(kids)):
+                assert np.array_equal(got[i], kids[i]), (mode, i)
+        finally:
+            ctx.close()

@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 import variants as V
-from golden_cases import IMAGES, PRESET_IMAGES, apply
+from golden_cases import IMAGES, NATIVE_800, PRESET_IMAGES, apply
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-5
@@ -53,6 +53,18 @@ def test_golden_images(R, ctxs, golden_dir, case):
     img, st = ctx.render(cam, prm, W, H)
     assert st.rays == int(g["rays"])
     assert float(np.max(np.abs(img - g["img"]))) <= TOL
+
+
+@pytest.mark.parametrize("name,cfg", NATIVE_800, ids=[n for n, _ in NATIVE_800])
+def test_native_800_frames(R, ctxs, golden_dir, name, cfg):
+    """C1, C2 and C5 at renderRayTracing's native 800x800 (src/main.cpp:33) against the oracle's whole
+    frames (tests/golden/native800.npz): every pixel within TOL, the same ray count."""
+    z = np.load(f"{golden_dir}/native800.npz")
+    _, ctx, prm, _, _ = ctxs(cfg)
+    cam = R.camera_from_trackball(aspect=1.0)
+    img, st = ctx.render(cam, prm, 800, 800)
+    assert st.rays == int(z[f"{name}__rays"])
+    assert float(np.max(np.abs(img - z[f"{name}__img"]))) <= TOL
 
 
 @pytest.mark.parametrize("case", PRESET_IMAGES, ids=[c[0] for c in PRESET_IMAGES])

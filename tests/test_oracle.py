@@ -5,7 +5,7 @@ output (render.bmp) is tests/test_render_bmp_pin.py."""
 import numpy as np
 import pytest
 
-from golden_cases import IMAGES, PRESET_IMAGES, apply
+from golden_cases import IMAGES, NATIVE_800, PRESET_IMAGES, REF_BVH_SCENES, apply
 
 
 def golden_images(golden_dir):
@@ -87,3 +87,49 @@ def test_ray_counts_split(R, O):
     assert int(rays.sum()) == total
     flipped = img.reshape(H, W, 3)[::-1].reshape(-1, 3)
     assert rgb.tobytes() == flipped.tobytes()
+
+
+def ref_bvh_fixture(golden_dir, cfg):
+    z = np.load(f"{golden_dir}/ref_bvh.npz")
+    off = z[f"{cfg}__offsets"]
+    ch = z[f"{cfg}__children"]
+    kids = [ch[off[i]:off[i + 1]] for i in range(len(off) - 1)]
+    return z[f"{cfg}__boxes"], z[f"{cfg}__is_leaf"], kids
+
+
+@pytest.mark.parametrize("cfg", REF_BVH_SCENES)
+def test_oracle_ref_bvh_matches_fixture(R, O, golden_dir, cfg):
+    """constructBVH's depth-4 median BVH (src/bounding_volume_hierarchy.cpp:108-217) of cube, monkey and
+    Cornell: node boxes bit for bit, leaf flags and every node's stored children (BFS node indices, a leaf's
+    objects in stored order) -- the dump tests/test_gpu_build.py holds the host and GPU builders to."""
+    boxes, leaf, kids = ref_bvh_fixture(golden_dir, cfg)
+    scene, _, _, _, _ = R.build_config(cfg)
+    orc = O.Oracle(scene)
+    b, l = orc.bvh_nodes()
+    assert b.tobytes() == boxes.tobytes()
+    assert np.array_equal(l, leaf)
+    for i in range(len(b)):
+        assert np.array_equal(orc.bvh_children(i), kids[i]), i
+    # structure: BFS creation order, <= 16 leaves at depth <= 4, every object in exactly one leaf
+    objs = np.concatenate([kids[i] for i in range(len(b)) if leaf[i]])
+    d = scene.desc()
+    assert np.array_equal(np.sort(objs), np.arange(d.num_triangles + d.num_spheres))
+    assert int(leaf.sum()) <= 16
+
+
+def native_fixture(golden_dir):
+    z = np.load(f"{golden_dir}/native800.npz")
+    return {n: (z[f"{n}__img"], int(z[f"{n}__rays"])) for n, _ in NATIVE_800}
+
+
+@pytest.mark.parametrize("name,cfg", NATIVE_800, ids=[n for n, _ in NATIVE_800])
+def test_oracle_native_800_sampled(R, O, golden_dir, name, cfg):
+    """renderRayTracing's native 800x800 frames (src/main.cpp:33): 2 048 pixels of each re-rendered by the
+    oracle bit for bit (the GPU renders the whole frame in test_gpu_parity.py)."""
+    img, _ = native_fixture(golden_dir)[name]
+    scene, prm, _, _, _ = R.build_config(cfg)
+    sel = np.random.default_rng(800).permutation(800 * 800)[:2048]
+    xy = np.stack([sel % 800, sel // 800], axis=1).astype(np.int32)
+    got, _ = O.Oracle(scene).render_pixels(prm, 800, 800, xy)
+    ref = img.reshape(800, 800, 3)[::-1].reshape(-1, 3)[sel]  # setPixel rows are top-first
+    assert got.reshape(-1, 3).tobytes() == ref.tobytes()

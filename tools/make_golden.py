@@ -5,7 +5,9 @@ be built here, so these vectors are produced by the restatement itself: they pin
 (regression) and are what the GPU parity tests compare against.  The oracle itself is pinned to
 the reference's render.bmp (tests/test_render_bmp_pin.py).  Re-run after an intentional semantic change:
 
-    python tools/make_golden.py
+    python tools/make_golden.py              # images.npz, kats.npz
+    python tools/make_golden.py --ref-bvh    # ref_bvh.npz
+    python tools/make_golden.py --native800  # native800.npz
 """
 import os
 import sys
@@ -21,7 +23,7 @@ import rt_amd as R  # noqa: E402
 
 OUT = os.path.join(REPO, "tests", "golden")
 
-from golden_cases import IMAGES, PRESET_IMAGES, apply  # noqa: E402
+from golden_cases import IMAGES, NATIVE_800, PRESET_IMAGES, REF_BVH_SCENES, apply  # noqa: E402
 
 
 def render_case(scene, prm, W, H):
@@ -69,7 +71,44 @@ def kat_rays(scene, n, seed):
     return rays
 
 
+def ref_bvh_dumps():
+    """tests/golden/ref_bvh.npz: the reference depth-4 BVH (constructBVH, src/bounding_volume_hierarchy.cpp:108-217)
+    of each scene as the oracle builds it -- node boxes (BFS creation order), leaf flags and every node's stored
+    children (node indices, or a leaf's objects in stored order: triangles by scene index, spheres as
+    num_triangles + sphere index), flattened with offsets."""
+    out = {}
+    for cfg in REF_BVH_SCENES:
+        scene, _, _, _, _ = R.build_config(cfg)
+        orc = O.Oracle(scene)
+        boxes, leaf = orc.bvh_nodes()
+        kids = [orc.bvh_children(i) for i in range(len(boxes))]
+        off = np.cumsum([0] + [len(k) for k in kids]).astype(np.int32)
+        out[f"{cfg}__boxes"] = boxes
+        out[f"{cfg}__is_leaf"] = leaf
+        out[f"{cfg}__children"] = np.concatenate(kids).astype(np.int32)
+        out[f"{cfg}__offsets"] = off
+        print(cfg, "ref BVH nodes", len(boxes), "leaves", int(leaf.sum()))
+    np.savez_compressed(os.path.join(OUT, "ref_bvh.npz"), **out)
+
+
+def native_800():
+    """tests/golden/native800.npz: C1, C2 and C5 at renderRayTracing's native 800x800 (src/main.cpp:33)."""
+    out = {}
+    O.set_threads(os.cpu_count() or 1)
+    for name, cfg in NATIVE_800:
+        scene, prm, _, _, _ = R.build_config(cfg)
+        img, rays = render_case(scene, prm, 800, 800)
+        out[f"{name}__img"] = img
+        out[f"{name}__rays"] = np.uint64(rays)
+        print(name, rays, float(img.max()))
+    np.savez_compressed(os.path.join(OUT, "native800.npz"), **out)
+
+
 def main():
+    if "--ref-bvh" in sys.argv:
+        return ref_bvh_dumps()
+    if "--native800" in sys.argv:
+        return native_800()
     os.makedirs(OUT, exist_ok=True)
     images = {}
     for name, cfg, W, H, uv, over in IMAGES:
