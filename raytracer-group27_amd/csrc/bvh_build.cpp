@@ -790,6 +790,7 @@ Bvh8 build_bvh8(const Bvh2& b2, int width) {
                         lo[a] = std::min(lo[a], c.lo[a]);
                         hi[a] = std::max(hi[a], c.hi[a]);
                     }
+                const int axis = slot_order(ch.data(), (int)ch.size(), lo, hi);
                 int e[3];
                 for (int a = 0; a < 3; ++a) {
                     std::memcpy(&w[a], &lo[a], 4);
@@ -806,7 +807,8 @@ Bvh8 build_bvh8(const Bvh2& b2, int width) {
                     if (ex > 40) err[j] = "BVH8: scene extent too large to quantise";
                     e[a] = ex;
                 }
-                w[3] = (uint32_t)(e[0] + 127) | ((uint32_t)(e[1] + 127) << 8) | ((uint32_t)(e[2] + 127) << 16);
+                w[3] = (uint32_t)(e[0] + 127) | ((uint32_t)(e[1] + 127) << 8) | ((uint32_t)(e[2] + 127) << 16) |
+                       ((uint32_t)axis << 24);
                 uint32_t imask = 0, lmask = 0, counts = 0;
                 uint16_t q[6][8];
                 for (int sl = 0; sl < 8; ++sl)

@@ -81,4 +81,36 @@ Bvh8 build_bvh8(const Bvh2& b2, int width = 8);
 // f(begin, end) over [0, n) in chunks of `chunk`, on the host's threads (scene upload loops)
 void parallel_chunks(int n, int chunk, const std::function<void(int, int)>& f);
 
+// BVH8 slot order, one rule for both builders (bvh_build.cpp build_bvh8, rt_build.hip k_collapse): the
+// inner children first, sorted by the centre of their boxes (lo + hi) along the node's longest axis
+// (stable), then the leaves in collapse order.  With the inner children in the low slots a child's node
+// index is child_base + slot, so a traversal can take the next child of a stacked group without reading
+// the parent node again, and the axis (returned; node word 3, bits 24-25) lets it take a group's children
+// front to back along the ray's direction.  Slot order never changes a result, only the work.
+template <class C>
+RT_HD int slot_order(C* ch, int n, const float lo[3], const float hi[3]) {
+    int axis = 0;
+    float ext = hi[0] - lo[0];
+    for (int a = 1; a < 3; ++a)
+        if (hi[a] - lo[a] > ext) {
+            ext = hi[a] - lo[a];
+            axis = a;
+        }
+    for (int i = 1; i < n; ++i) {  // insertion sort (n <= 8), stable
+        const C x = ch[i];
+        const bool xl = x.count > 0;
+        const float xc = x.lo[axis] + x.hi[axis];
+        int j = i - 1;
+        while (j >= 0) {
+            const bool yl = ch[j].count > 0;
+            const float yc = ch[j].lo[axis] + ch[j].hi[axis];
+            if (!((!xl && yl) || (!xl && !yl && xc < yc))) break;
+            ch[j + 1] = ch[j];
+            --j;
+        }
+        ch[j + 1] = x;
+    }
+    return axis;
+}
+
 }  // namespace rt

@@ -901,6 +901,7 @@ __global__ void k_collapse(const Item8* __restrict__ items, int m, const Bvh2Nod
             lo[a] = fminf(lo[a], ch[i].lo[a]);
             hi[a] = fmaxf(hi[a], ch[i].hi[a]);
         }
+    const int axis = slot_order(ch, nch, lo, hi);
     int e[3];
     for (int a = 0; a < 3; ++a) {
         wl[a] = __float_as_uint(lo[a]);
@@ -915,7 +916,8 @@ __global__ void k_collapse(const Item8* __restrict__ items, int m, const Bvh2Nod
         if (ex > 40) atomicOr(err, 4);
         e[a] = ex;
     }
-    wl[3] = (uint32_t)(e[0] + 127) | ((uint32_t)(e[1] + 127) << 8) | ((uint32_t)(e[2] + 127) << 16);
+    wl[3] = (uint32_t)(e[0] + 127) | ((uint32_t)(e[1] + 127) << 8) | ((uint32_t)(e[2] + 127) << 16) |
+            ((uint32_t)axis << 24);
     uint32_t imask = 0, lmask = 0, cnts = 0;
     uint32_t q[6][8];
     for (int sl = 0; sl < 8; ++sl)

@@ -12,3 +12,4 @@ void set_error(const std::string& msg);
                                // the 800k-triangle dragon proxy has depth 7); deeper trees run the whole-traversal kernel
 #define RT_MAX_REF_NODES 31    // depth-4 binary reference BVH
 #define RT_WAVE 64
+#define RT_STATS_EXTRA (16 + 8 * 16)  // d_stats: 16 counters, the 8 per-XCD job heads, then 16 more counters

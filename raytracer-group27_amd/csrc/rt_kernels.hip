@@ -151,6 +151,9 @@ struct Cnt {
     unsigned long long cyc_a, cyc_b;  // shader clocks per wave in the state machine / in traversal (df kernel)
     unsigned long long cyc_c, cyc_d;  // ... of cyc_a: advancing finished queries / fetching jobs
     uint32_t hist[3];  // df kernel traversal iterations by tracing lanes 1-16 / 17-32 / 33-64 (leader)
+    // node visits that re-test a node popped from the stack (slot mask < 0xFF), the popped groups' slot
+    // counts and how many of those slots still hit (counting builds: the cost of the re-visit scheme)
+    uint32_t rv, rvk, rvj;
 };
 
 // true on the lowest active lane of the wave (counting builds: one count per wave instruction stream)
@@ -574,6 +577,12 @@ __device__ void flush_counters(const KParams& P, const Cnt& c) {
             unsigned long long v = c.hist[k];
             for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
             if ((threadIdx.x & 63) == 0) atomicAdd(P.stats + 13 + k, v);
+        }
+        const uint32_t xs[3] = {c.rv, c.rvk, c.rvj};
+        for (int k = 0; k < 3; ++k) {
+            unsigned long long v = xs[k];
+            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+            if ((threadIdx.x & 63) == 0) atomicAdd(P.stats + RT_STATS_EXTRA + k, v);
         }
     }
 }

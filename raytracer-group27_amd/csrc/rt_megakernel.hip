@@ -991,6 +991,7 @@ __device__ __attribute__((noinline)) bool advance_lane_call(const void* ka, Lane
 #define RT_V_FAN 256  // dynamic fetch: the spherical-light sample fans compiled in (P.fan)
 
 #define RT_V_W3 8    // compiled for 3 waves per SIMD (168 VGPRs)
+#define RT_V_REVISIT 32  // opaque / tree kernels: the re-visit group stack of the other kernels (A/B), not DIRECT
 #define RT_V_WAVES(V) (((V) & RT_V_W4) ? 4 : ((V) & RT_V_W3) ? 3 : 2)
 
 
@@ -1161,7 +1162,12 @@ __device__ __forceinline__ void node_fetch(const float4* nodes, uint32_t cur, fl
 // at once into g), and the hit leaf slots postponed into T.lb/lc/lh.
 // PF: the node was prefetched into g by the previous visit (and the next one is prefetched here);
 // otherwise it is loaded now (fewer live registers).
-template <bool COUNT, int NW, bool PF = true>
+// DIRECT (the opaque and tree kernels): the stack holds groups of children, (child_base << 9) | (order << 8) |
+// slots (the builders put the inner children in the low slots, bvh_build.h slot_order, so a child's node is
+// child_base + slot), and a pop takes the group's next child at once -- front to back along the node's sort
+// axis by the ray's direction (order bit) -- where the re-visit form (node << 8) | slots re-tests the parent's
+// remaining slots first (one more node visit per pop).  Either walk gives the same lexicographic minimum.
+template <bool COUNT, int NW, bool PF = true, bool DIRECT = false>
 __device__ __forceinline__ void trav_node(const DevScene& S, Trav& T, int* stk, float4 (&g)[8], Cnt& cnt) {
     const uint32_t node = T.cur >> 8;
     if (!PF) node_fetch(S.nodes, T.cur, g);
@@ -1215,18 +1221,44 @@ __device__ __forceinline__ void trav_node(const DevScene& S, Trav& T, int* stk, 
     T.lc = __float_as_uint(f1.w);
     T.lh = hits & lmask;
     const uint32_t ih = hits & imask;
+    if (COUNT && (T.cur & 0xFFu) != 0xFFu) {
+        cnt.rv++;
+        cnt.rvk += __popc(T.cur & 0xFFu);
+        cnt.rvj += __popc(ih);
+    }
     if (ih) {
         const uint32_t sbest = kbest & 7u;
         const uint32_t rest = ih & ~(1u << sbest);
-        if (rest) {
-            stk[T.sp * RT_WAVE] = (int)((node << 8) | rest);
-            ++T.sp;
+        if (DIRECT) {
+            if (rest) {
+                const uint32_t ax = (w3 >> 24) & 3u;
+                const uint32_t back = ax == 0u ? (uint32_t)sx : ax == 1u ? (uint32_t)sy : (uint32_t)sz;
+                stk[T.sp * RT_WAVE] = (int)((child_base << 9) | (back << 8) | rest);
+                ++T.sp;
+            }
+            T.cur = ((child_base + sbest) << 8) | 0xFFu;
+        } else {
+            if (rest) {
+                stk[T.sp * RT_WAVE] = (int)((node << 8) | rest);
+                ++T.sp;
+            }
+            const uint32_t rank = __popc(imask & ((1u << sbest) - 1u));
+            T.cur = ((child_base + rank) << 8) | 0xFFu;
         }
-        const uint32_t rank = __popc(imask & ((1u << sbest) - 1u));
-        T.cur = ((child_base + rank) << 8) | 0xFFu;
     } else if (T.sp > 0) {
-        --T.sp;
-        T.cur = (uint32_t)stk[T.sp * RT_WAVE];
+        if (DIRECT) {
+            // the group's next child: the lowest slot along the axis, or the highest for a ray going back
+            const uint32_t e = (uint32_t)stk[(T.sp - 1) * RT_WAVE];
+            const uint32_t m = e & 0xFFu;
+            const uint32_t sl = (e & 0x100u) ? 31u - __clz(m) : (uint32_t)(__ffs(m) - 1);
+            const uint32_t left = m & ~(1u << sl);
+            if (left) stk[(T.sp - 1) * RT_WAVE] = (int)((e & ~0xFFu) | left);
+            else --T.sp;
+            T.cur = (((e >> 9) + sl) << 8) | 0xFFu;
+        } else {
+            --T.sp;
+            T.cur = (uint32_t)stk[T.sp * RT_WAVE];
+        }
     } else {
         T.cur = RT_TRAV_NONE;
     }
@@ -1582,6 +1614,23 @@ __device__ __attribute__((noinline)) uint4 coop_group_trace_call(const float4* _
                                                                  const int* __restrict__ leaf_path, int* pool, int* q,
                                                                  unsigned long long om, int reserve) {
     return coop_group_trace<NW>(nodes, tri, refn, leaf_path, pool, q, om, reserve);
+}
+
+// DIRECT stacks (trav_node): the pool entries the lane groups take, one per pending child, (node << 8) | 0xFF,
+// then the node about to be visited; returns the count.  direct_pending counts them without writing.
+__device__ __forceinline__ int direct_pending(const Trav& T, const int* stk) {
+    int n = T.cur != RT_TRAV_NONE ? 1 : 0;
+    for (int j = 0; j < T.sp; ++j) n += __popc((uint32_t)stk[j * RT_WAVE] & 0xFFu);
+    return n;
+}
+__device__ __forceinline__ int direct_to_pool(const Trav& T, const int* stk, int* gp) {
+    int n = 0;
+    for (int j = 0; j < T.sp; ++j) {
+        const uint32_t e = (uint32_t)stk[j * RT_WAVE];
+        for (uint32_t m = e & 0xFFu; m; m &= m - 1u) gp[n++] = (int)((((e >> 9) + (uint32_t)(__ffs(m) - 1)) << 8) | 0xFFu);
+    }
+    if (T.cur != RT_TRAV_NONE) gp[n++] = (int)T.cur;
+    return n;
 }
 
 // Epilogue of trace_query8: the spheres, after every triangle (same order and keys).
@@ -2203,7 +2252,7 @@ __device__ __forceinline__ bool lite_advance(const KParams& P, LiteLane& L, bool
 
 template <bool COUNT, int V>
 __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KParams, JobSrc) {
-    constexpr bool PF = !(V & RT_V_NOPF), COOP = !(V & RT_V_NOCOOP);
+    constexpr bool PF = !(V & RT_V_NOPF), COOP = !(V & RT_V_NOCOOP), DIRECT = !(V & RT_V_REVISIT);
     // the kernel's arguments are read where each phase uses them (fresh_kernarg), not held in SGPRs
     const void* ka = (const void*)__builtin_amdgcn_kernarg_segment_ptr();
 #define RT_FRESH const KParams& P = *(const KParams*)fresh_kernarg(ka); const DevScene& S = P.S
@@ -2323,7 +2372,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
                 const bool rec = leaf_pending(T);
                 if (rec) trav_record<COUNT, true>(S, T, cnt);
                 const bool nv = T.cur != RT_TRAV_NONE && (!rec || (P.dual && T.lh == 0u));
-                if (nv) trav_node<COUNT, 8, PF>(S, T, stk, g, cnt);
+                if (nv) trav_node<COUNT, 8, PF, DIRECT>(S, T, stk, g, cnt);
             }
             if (tracing && !leaf_pending(T) && T.cur == RT_TRAV_NONE) {
                 trav_finish(S, T);
@@ -2340,9 +2389,17 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
             // drain (no lane can take a new job): the wave's last queries walked by lane groups, as in
             // persistent_df_kernel (coop 2: also the last ones a full-wave refill waits for).  The lane
             // groups run after the loop, so their registers do not add to the traversal loop's
-            if (COOP && P.coop && (P.coop == 2 || (!__any(L.job == -1) && __any(L.job == -2))) &&
-                __popcll(__ballot(tracing)) <= P.coop_max)
-                break;
+            if (COOP && P.coop && (P.coop == 2 || (!__any(L.job == -1) && __any(L.job == -2)))) {
+                const int ntr = __popcll(__ballot(tracing));
+                if (ntr <= P.coop_max) {
+                    if (!DIRECT) break;
+                    // a DIRECT stack expands into one pool entry per pending child: the groups take the
+                    // queries once every one fits its share of the pool above the depth-first reserve
+                    int G = 64;
+                    while (G > 1 && ntr * G > 64) G >>= 1;
+                    if (!__any(tracing && direct_pending(T, stk) > COOP_POOL * G / 64 - P.coop_reserve)) break;
+                }
+            }
         }
         if (COOP && __any(tracing)) {
             const unsigned long long om = __ballot(tracing);
@@ -2353,8 +2410,12 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
             if (tracing) {
                 coop_put(T, coop_q, r);
                 int* gp = coop_pool + r * (COOP_POOL * G / 64);
-                for (int j = 0; j < T.sp; ++j) gp[j] = stk[j * RT_WAVE];
-                if (T.cur != RT_TRAV_NONE) gp[T.sp] = (int)T.cur;
+                if (DIRECT) {
+                    coop_q[CQ_TOP * COOP_Q + r] = direct_to_pool(T, stk, gp);
+                } else {
+                    for (int j = 0; j < T.sp; ++j) gp[j] = stk[j * RT_WAVE];
+                    if (T.cur != RT_TRAV_NONE) gp[T.sp] = (int)T.cur;
+                }
             }
             __syncthreads();
             const uint4 nv =
@@ -2657,7 +2718,7 @@ __device__ __forceinline__ int tree_advance(const KParams& P, TreeLane& L, int v
 
 template <bool COUNT, int V>
 __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_tree_kernel(KParams, JobSrc) {
-    constexpr bool PF = !(V & RT_V_NOPF);
+    constexpr bool PF = !(V & RT_V_NOPF), DIRECT = !(V & RT_V_REVISIT);
     const void* ka = (const void*)__builtin_amdgcn_kernarg_segment_ptr();
 #define RT_FRESH const KParams& P = *(const KParams*)fresh_kernarg(ka); const DevScene& S = P.S
     __shared__ int stack_lds[RT_STACK8 * RT_WAVE];
@@ -2897,7 +2958,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_tree_kernel(KPar
                 const bool rec = leaf_pending(T);
                 if (rec) trav_record<COUNT, true>(S, T, cnt);
                 const bool nv = T.cur != RT_TRAV_NONE && (!rec || (P.dual && T.lh == 0u));
-                if (nv) trav_node<COUNT, 8, PF>(S, T, stk, g, cnt);
+                if (nv) trav_node<COUNT, 8, PF, DIRECT>(S, T, stk, g, cnt);
             }
             if (tracing && !leaf_pending(T) && T.cur == RT_TRAV_NONE) {
                 trav_finish(S, T);

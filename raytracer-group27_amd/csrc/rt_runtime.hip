@@ -134,7 +134,7 @@ struct rt_ctx {
     int opt_dual = -1;        // dynamic-fetch steps: record and node visit in one iteration (-1 default, 0 off, 1 on)
     int opt_variant = -1;   // -1: the shipped variant for the render shape (RT_DF_BATCH / _FRAME, RT_WT_DEFAULT)
     int opt_opaque = -1;    // opaque-scene kernel: -1 where eligible (build by render shape), 0 never, 1 / 2 the 4- / 3-wave build
-    int opt_tree = -1;      // recursion-tree kernel: -1 where eligible (build by render shape), 0 never, 1 / 2 the 4- / 3-wave build
+    int opt_tree = -1;      // recursion-tree kernel: -1 / 2 where eligible, 0 never, 1 its re-visit group stack build (A/B)
     char last_kernel[64] = {0};
     // view batches: the camera table's pinned host staging and the event of its last copy (the buffer
     // is refilled only once that copy has read it)
@@ -212,7 +212,7 @@ static void build_texels(const rt_texture& t, std::vector<float>& out, int& leve
 }
 
 // d_stats: 16 counters, then the 8 per-XCD job heads (128-B apart) of the dynamic-fetch kernel
-#define RT_STATS_BYTES ((16 + 8 * 16) * sizeof(unsigned long long))
+#define RT_STATS_BYTES ((RT_STATS_EXTRA + 16) * sizeof(unsigned long long))
 
 #define HIP_TRY(expr)                                                                           \
     do {                                                                                        \
@@ -503,6 +503,7 @@ static int create_one(const rt_scene_desc* desc, int device, rt_ctx** out) {
         return RT_ERR_INVALID;
     }
     c->nnodes = gpu_built ? gbuild.nnodes : (int)(bvh8.nodes.size() / 32);
+    if (c->nnodes >= (1 << 23)) c->df_ok = false;  // the DIRECT group stack's entries hold child_base << 9
     c->nrec = ntri;
 
     // --- triangle records (64 B) in BVH8 leaf order: v0|n.x, v1|n.y, v2|n.z, D|key_brute|key_bvh|ref_leaf ---
@@ -918,7 +919,7 @@ static int set_option_one(rt_ctx* c, int option, int value) {
             c->opt_variant = value;
             return RT_OK;
         case RT_OPT_OPAQUE:
-            if (value < -1 || value > 2) break;
+            if (value < -1 || value > 3) break;
             c->opt_opaque = value;
             return RT_OK;
         case RT_OPT_TREE:
@@ -997,12 +998,14 @@ static bool opaque_path(const rt_ctx* c, const KParams& K, bool pixels) {
 }
 // the opaque kernel's 3-wave build: single frames (RT_OPT_OPAQUE 1 / 2 force the 4- / 3-wave build)
 static bool opaque_w3(const rt_ctx* c, const KParams& K) {
-    return c->opt_opaque == 2 || (c->opt_opaque != 1 && K.n_views <= 1);
+    return c->opt_opaque == 2 || (c->opt_opaque != 1 && c->opt_opaque != 3 && K.n_views <= 1);
 }
 
 // the recursion-tree kernel (rt_megakernel.hip persistent_tree_kernel): 4 / 3 waves per SIMD
-#define RT_TREE_V (RT_V_W4 | RT_V_NOPF)
+// One build, 3 waves per SIMD, for frames and batches: the 4-wave build (67 spilled VGPRs) faulted on the
+// C4 16-view batch at full size (round 4, gpurun_out/bench_r04b_C4.json) and is not compiled.
 #define RT_TREE_V3 (RT_V_W3 | RT_V_NOPF)
+#define RT_TREE_VR (RT_V_W3 | RT_V_NOPF | RT_V_REVISIT)  // A/B: the re-visit group stack (RT_OPT_TREE 1)
 
 // Renders that the recursion-tree kernel draws: pixels of a dynamic-fetch-class render the opaque kernel
 // does not take, without textures or glossy lobes, whose spherical and plane lights fit one fan (<= 64
@@ -1015,9 +1018,7 @@ static bool tree_path(const rt_ctx* c, const KParams& K, bool pixels) {
     if (K.S.nplane > 0 && K.plane_k * K.plane_k > 64) return false;
     return (long long)K.S.npl + K.S.nsl + K.S.nspot + K.S.nplane < 65536;  // TreeLane::li
 }
-static bool tree_w3(const rt_ctx* c, const KParams& K) {
-    return c->opt_tree == 2 || (c->opt_tree != 1 && K.n_views <= 1);
-}
+static int tree_variant(const rt_ctx* c) { return c->opt_tree == 1 ? RT_TREE_VR : RT_TREE_V3; }
 
 // by render shape: view batches and sample-fan renders run the lean 4-wave variant (C4 single frame
 // with fans: 27.1 vs 30.3 ms), other single frames the 2-wave variant with the drain lane groups
@@ -1050,18 +1051,26 @@ template <bool COUNT>
 static int launch_persistent(int grid, hipStream_t st, const KParams& K, const JobSrc& J, rt_ctx* c) {
     if (opaque_path(c, K, J.mode == 0)) {
         const bool w3 = opaque_w3(c, K);
-        if (w3) hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V3>), dim3(grid), dim3(64), 0, st, K, J);
-        else hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V>), dim3(grid), dim3(64), 0, st, K, J);
+        int v = w3 ? RT_OPAQUE_V3 : RT_OPAQUE_V;
+        if (c->opt_opaque == 3) {  // A/B: the 4-wave build with the re-visit group stack
+            v = RT_OPAQUE_V | RT_V_REVISIT;
+            hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V | RT_V_REVISIT>), dim3(grid), dim3(64), 0, st,
+                               K, J);
+        } else if (w3) {
+            hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V3>), dim3(grid), dim3(64), 0, st, K, J);
+        } else {
+            hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V>), dim3(grid), dim3(64), 0, st, K, J);
+        }
         std::snprintf(c->last_kernel, sizeof(c->last_kernel), "rt::persistent_opaque_kernel<%s, %d>",
-                      COUNT ? "true" : "false", w3 ? RT_OPAQUE_V3 : RT_OPAQUE_V);
+                      COUNT ? "true" : "false", v);
         return RT_OK;
     }
     if (tree_path(c, K, J.mode == 0)) {
-        const bool w3 = tree_w3(c, K);
-        if (w3) hipLaunchKernelGGL((persistent_tree_kernel<COUNT, RT_TREE_V3>), dim3(grid), dim3(64), 0, st, K, J);
-        else hipLaunchKernelGGL((persistent_tree_kernel<COUNT, RT_TREE_V>), dim3(grid), dim3(64), 0, st, K, J);
+        const int v = tree_variant(c);
+        if (v == RT_TREE_VR) hipLaunchKernelGGL((persistent_tree_kernel<COUNT, RT_TREE_VR>), dim3(grid), dim3(64), 0, st, K, J);
+        else hipLaunchKernelGGL((persistent_tree_kernel<COUNT, RT_TREE_V3>), dim3(grid), dim3(64), 0, st, K, J);
         std::snprintf(c->last_kernel, sizeof(c->last_kernel), "rt::persistent_tree_kernel<%s, %d>",
-                      COUNT ? "true" : "false", w3 ? RT_TREE_V3 : RT_TREE_V);
+                      COUNT ? "true" : "false", v);
         return RT_OK;
     }
     const bool df = use_df(c, K);
@@ -1107,13 +1116,13 @@ static int persistent_grid(rt_ctx* c, const KParams& K, bool pixels) {
         return c->opaque_blocks[key];
     }
     if (tree_path(c, K, pixels)) {
-        const int key = tree_w3(c, K) ? 1 : 0;
+        const int key = tree_variant(c) == RT_TREE_VR ? 1 : 0;
         if (c->tree_blocks[key] > 0) return c->tree_blocks[key];
         int cus = 0, per_cu = 0;
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
         const hipError_t e =
-            key ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_tree_kernel<false, RT_TREE_V3>, 64, 0)
-                : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_tree_kernel<false, RT_TREE_V>, 64, 0);
+            key ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_tree_kernel<false, RT_TREE_VR>, 64, 0)
+                : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_tree_kernel<false, RT_TREE_V3>, 64, 0);
         if (e != hipSuccess || per_cu <= 0) per_cu = 8;
         c->tree_blocks[key] = std::max(1, cus) * per_cu;
         return c->tree_blocks[key];
@@ -1788,9 +1797,9 @@ extern "C" int rt_texture_sample(rt_ctx* c, int texture, int n, const float* uv_
 // Developer counters of the last counting launch ([8..11] state-machine / traversal clocks).
 extern "C" int rt_debug_counters(rt_ctx* c, uint64_t* out, int n) {
     if (!c || !out || n <= 0) return RT_ERR_INVALID;
-    unsigned long long h[16] = {0};
+    unsigned long long h[RT_STATS_EXTRA + 16] = {0};
     HIP_TRY(hipMemcpy(h, c->d_stats, sizeof(h), hipMemcpyDeviceToHost));
-    for (int i = 0; i < n && i < 16; ++i) out[i] = h[i];
+    for (int i = 0; i < n && i < 32; ++i) out[i] = h[i < 16 ? i : RT_STATS_EXTRA + i - 16];
     return RT_OK;
 }
 

@@ -9,6 +9,7 @@ import ctypes as C
 import gzip
 import os
 import shutil
+import sys as _sys
 import tempfile
 
 import numpy as np
@@ -155,7 +156,7 @@ OPT_DUAL_STEP = 10
 OPT_CENTRE_FIRST = 12  # job order: upper-half XCD tile ranges walked bottom-up (-1 by shape, 0 off, 1 on)
 OPT_OPAQUE = 11  # opaque-scene kernel: -1 where eligible (default), 0 the general kernels, 1 / 2 the 4- / 3-wave build
 OPT_PEER_STORES = 14  # split renders: -1 peer stores where peer access works (default), 0 band-dense + copy always
-OPT_TREE = 13  # recursion-tree kernel (C4 / C5 class): -1 where eligible (default), 0 the general kernels, 1 / 2 the 4- / 3-wave build
+OPT_TREE = 13  # recursion-tree kernel (C4 / C5 class): -1 / 2 where eligible (default), 0 the general kernels, 1 its re-visit group stack build (A/B)
 KERNEL_AUTO, KERNEL_WHOLE_TRAVERSAL, KERNEL_DYNAMIC_FETCH = 0, 1, 2
 # compiled kernel variants (rt_megakernel.hip RT_V_*, rt_runtime.hip RT_DF_* / RT_WT_*)
 V_CALL, V_NOPF, V_NOCOOP, V_W4 = 1, 2, 4, 16
@@ -505,11 +506,13 @@ class Context:
     def __del__(self):
         # nothing during interpreter shutdown: HIP's own teardown may already have run, and destroying
         # device resources after it can hang or fault the process -- close() contexts explicitly
-        import sys as _sys
-
-        if getattr(_sys, "is_finalizing", lambda: False)() or not callable(lib):
-            return
-        self.close()
+        # (module-level sys: an import inside __del__ itself fails once shutdown has begun)
+        try:
+            if _sys.is_finalizing() or not callable(lib):
+                return
+            self.close()
+        except Exception:  # noqa: BLE001 -- a destructor must not raise
+            pass
 
     def create_ms(self):
         """rt_create's cumulative phase clock (ms): device, ref BVH, BVH2/8, records, materials, uploads, total."""
@@ -540,8 +543,10 @@ class Context:
         obj_leaf = np.zeros(max(nobj, 1), np.int32)
         obj_key = np.zeros(max(nobj, 1), np.int32)
         ip = lambda a: a.ctypes.data_as(C.POINTER(C.c_int))  # noqa: E731
-        check(lib().rt_debug_ref_bvh(self.h, boxes.ctypes.data_as(C.POINTER(C.c_float)), ip(node_leaf), ip(obj_leaf),
-                                     ip(obj_key)), "rt_debug_ref_bvh")
+        rc = lib().rt_debug_ref_bvh(self.h, boxes.ctypes.data_as(C.POINTER(C.c_float)), ip(node_leaf), ip(obj_leaf),
+                                    ip(obj_key))
+        if rc < 0:  # (returns the node count)
+            check(rc, "rt_debug_ref_bvh")
         boxes, node_leaf, obj_leaf, obj_key = boxes[:nref], node_leaf[:nref], obj_leaf[:nobj], obj_key[:nobj]
         children, nxt = [], 1
         for i in range(nref):
@@ -657,8 +662,8 @@ class Context:
               "rt_update_materials")
 
     def debug_counters(self):
-        out = np.zeros(16, np.uint64)
-        check(lib().rt_debug_counters(self.h, out.ctypes.data_as(C.POINTER(C.c_uint64)), 16))
+        out = np.zeros(32, np.uint64)
+        check(lib().rt_debug_counters(self.h, out.ctypes.data_as(C.POINTER(C.c_uint64)), 32))
         return out
 
     def selftest_math(self, x, y):

@@ -85,7 +85,8 @@ def test_builders_reproduce_reference_bvh_dump(cfg, golden_dir):
     kids = [ch[off[i]:off[i + 1]] for i in range(len(off) - 1)]
     boxes, leaf = z[f"{cfg}__boxes"], z[f"{cfg}__is_leaf"]
     s, _, _, _, _ = R.build_config(cfg)
-    for mode in (R.BUILD_HOST, R.BUILD_GPU):
+    # (the GPU build takes scenes of >= 16 triangles: rt_build.hip; the cube has 12)
+    for mode in (R.BUILD_HOST, R.BUILD_GPU) if s.desc().num_triangles >= 16 else (R.BUILD_HOST,):
         ctx = _ctx(s, mode)
         try:
             b, node_leaf, got = ctx.ref_bvh()

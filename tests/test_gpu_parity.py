@@ -450,3 +450,40 @@ def test_bench_step_c3_64_views(R, O, ctxs):
     ref, _ = O.Oracle(scene).render_pixels(prm, W, H, xy, euler=eulers[21])
     print(f"bench step: oracle done {time.time() - t0:.2f} s", flush=True)
     assert float(np.max(np.abs(view[xy[:, 1], xy[:, 0]] - ref))) <= TOL
+
+
+def test_opaque_kernel_spot_lights(R, O):
+    """Spot lights through the opaque-scene kernel (lite_next_light's cone test and its point-then-spot
+    light order, rt_megakernel.hip) against the general kernels and the oracle: the dragon proxy lit by one
+    point light and two spot lights whose cones cut the object (src/shadow.cpp:228-247), so pixels inside
+    and outside each cone occur.  Every build of the opaque kernel (4-wave, 3-wave, the re-visit group
+    stack) renders the general kernels' bits and ray count."""
+    scene, prm, _, _, _ = R.build_config("C3", dragon_uv=(200, 80))
+    scene.clear_lights()
+    scene.add_point_light((-1, 1, -1), (0.5, 0.5, 0.5))
+    scene.add_spot_light((1, 1, -1), (-1, -1, 1), 20, (0.8, 0.6, 0.4))
+    scene.add_spot_light((0, 1.5, 0.2), (0, -1, -0.1), 10, (0.3, 0.3, 0.9))
+    W, H = 96, 54
+    ctx = R.Context(scene)
+    try:
+        cam = R.camera_from_trackball(aspect=R.aspect_of(W, H))
+        ref, rays = O.Oracle(scene).render(prm, W, H)
+        df = R.KERNEL_DYNAMIC_FETCH
+        base = None
+        for opaque in (0, 1, 2, 3):
+            with V.options(R, ctx, {R.OPT_KERNEL: df, R.OPT_OPAQUE: opaque}):
+                img, st = ctx.render(cam, prm, W, H)
+            assert ("opaque" in st.kernel_name) == (opaque != 0), (opaque, st.kernel_name)
+            assert st.rays == rays, opaque
+            assert float(np.max(np.abs(img - ref))) <= TOL, opaque
+            if base is None:
+                base = img
+            assert img.tobytes() == base.tobytes(), opaque
+        # the spot lights light part of the object: without them the image changes, but not everywhere
+        point_only, _, _, _, _ = R.build_config("C3", dragon_uv=(200, 80))
+        point_only.clear_lights()
+        point_only.add_point_light((-1, 1, -1), (0.5, 0.5, 0.5))
+        diff = np.any(O.Oracle(point_only).render(prm, W, H)[0].reshape(-1, 3) != ref.reshape(-1, 3), axis=1)
+        assert 0 < int(diff.sum()) < W * H
+    finally:
+        ctx.close()

@@ -6,12 +6,14 @@
 #
 # STEP                          what runs (outputs under gpurun_out/, TAG in the names)
 #   tests[:PYTEST_K]            pytest -m gpu (optionally -k PYTEST_K)
+#   testsall                    pytest -m gpu without -x (every failure in one session; ends the session if any)
 #   smoke                       __graft_entry__.smoke()
 #   bench[:CFG[:VIEWS]]         bench.py line (N = 1; roofline.traffic measured by its rocprofv3 passes)
 #   stats[:CFG[:VIEWS]]         rocprofv3 --kernel-trace --stats of bench.py (kernel summary for profiles/)
 #   pmc[:CFG[:VIEWS]]           the PMC counter groups of tools/pmc_counters.txt (tools/profile.sh)
 #   ab:CFGS:VIEWS:ROUNDS[:ARMS] tools/ab_variants.py (CFGS / ARMS comma-separated; ARMS name=k=v;k=v)
-#   simd[:CFG[:VIEWS]]          tools/simd_eff.py (counting build: lanes per node / record step)
+#   simd[:CFG[:VIEWS[:ARMS]]]   tools/simd_eff.py (counting build: lanes per node / record step; ARMS comma-separated
+#                               name@k=v, e.g. new@,old@11=3)
 #   wave[:CFG[:VIEWS[:COUNT]]]  tools/wave_trace.py (per-wave start / drain / end; COUNT 1: counting build)
 #   jobs[:CFG[:OPTS]]           tools/job_trace.py (per-pixel query chains of a single frame; OPTS k=v;k=v)
 #   ranks                       bench.py N = 2 on this one GPU (gloo control plane, IPC exchange)
@@ -37,6 +39,7 @@ for step in "$@"; do
   case $name in
     tests) if [ -n "$a" ]; then K=(-k "$a"); else K=(); fi
            run 1200 pytest_gpu_${TAG}.log python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${K[@]}" ;;
+    testsall) run 1200 pytest_gpu_${TAG}.log python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ;;
     smoke) run 300 smoke_${TAG}.log python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run 600 bench_${TAG}_${a:-C3}.json python bench.py --steps 20 --warmup 3 --config ${a:-C3} ${b:+--views $b} ;;
     stats) run 600 stats_${TAG}_${a:-C3}.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/stats_${TAG}_${a:-C3} -o run -- python3 bench.py --steps 20 --warmup 3 --config ${a:-C3} ${b:+--views $b} --no-cpu-baseline --no-single-frame --no-pmc
@@ -44,7 +47,7 @@ for step in "$@"; do
     pmc)   run 900 pmc_${TAG}_${a:-C3}.log bash tools/profile.sh ${TAG}_${a:-C3} ${a:-C3} ${b:-64} ;;
     ab)    ARMS=(); if [ -n "$d" ]; then for x in ${d//,/ }; do ARMS+=("${x//;/,}"); done; ARMS=(--arms "${ARMS[@]/=/:}"); fi
            run 900 ab_${TAG}.log python -u tools/ab_variants.py ${a//,/ } --views ${b:-16} --rounds ${c:-3} "${ARMS[@]}" ;;
-    simd)  run 300 simd_${TAG}.log env SE_VIEWS=${b:-16} python tools/simd_eff.py ${a:-C3} ;;
+    simd)  c=${c//,/ }; run 300 simd_${TAG}_${a:-C3}.log env SE_VIEWS=${b:-16} python tools/simd_eff.py ${a:-C3} ${c//@/:} ;;
     wave)  run 300 wave_${TAG}${c:+_count}.log env WT_VIEWS=${b:-1} WT_COUNT=${c:-0} python tools/wave_trace.py ${a:-C3} ;;
     jobs)  run 300 jobs_${TAG}${b:+_$b}.log python tools/job_trace.py ${a:-C3} ${b//;/ } ;;
     ranks) run 600 ranks_${TAG}.json env BENCH_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29555 bench.py --gpus 2 --steps 5 --warmup 1 --no-single-frame ;;

@@ -42,5 +42,8 @@ for cfg in cfgs:
               f"adv={wa / rays:.3f} cycA={int(c[8]) / max(1, int(c[8]) + int(c[9])):.2f} "
               f"(advance {int(c[10]) / max(1, int(c[8])):.2f}, job fetch {int(c[11]) / max(1, int(c[8])):.2f}) "
               f"iterations by tracing lanes 1-16/17-32/33-64: "
-              f"{[round(int(c[k]) / max(1, sum(int(c[j]) for j in (13, 14, 15))), 3) for k in (13, 14, 15)]}", flush=True)
+              f"{[round(int(c[k]) / max(1, sum(int(c[j]) for j in (13, 14, 15))), 3) for k in (13, 14, 15)]} "
+              f"revisits/ray={int(c[16]) / rays:.3f} (share of visits {int(c[16]) / max(1, nodes):.3f}, "
+              f"popped slots/revisit {int(c[17]) / max(1, int(c[16])):.2f}, still hit {int(c[18]) / max(1, int(c[16])):.2f})",
+              flush=True)
     ctx.close()
