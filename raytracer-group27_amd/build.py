@@ -32,7 +32,15 @@ def _stale(src, obj, deps):
     return any(os.path.getmtime(p) > t for p in [src] + deps)
 
 
-def build(force=False, verbose_resource=False):
+def build(force=False, verbose_resource=False, defines=(), out=None):
+    """defines / out (developer A/B builds, e.g. RT_MAX_LEAF=2): compiled into a separate object directory
+    and library, the in-tree librt_amd.so untouched."""
+    global BUILD, LIB
+    if defines or out:
+        tag = "_".join(d.replace("=", "") for d in defines) or "alt"
+        BUILD = os.path.join(HERE, "build", "ab_" + tag)
+        LIB = out or os.path.join(HERE, "build", f"lib_{tag}.so")
+    extra_d = [f"-D{d}" for d in defines]
     os.makedirs(BUILD, exist_ok=True)
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".h", ".hip"))]
     headers.append(os.path.join(HERE, "..", "include", "rt_amd.h"))
@@ -41,15 +49,15 @@ def build(force=False, verbose_resource=False):
         src = os.path.join(CSRC, s)
         obj = os.path.join(BUILD, s + ".o")
         if force or _stale(src, obj, headers):
-            _run(["g++"] + COMMON + ["-c", src, "-o", obj])
+            _run(["g++"] + COMMON + extra_d + ["-c", src, "-o", obj])
         objs.append(obj)
     for s in HIP_SRCS:
         src = os.path.join(CSRC, s)
         obj = os.path.join(BUILD, s + ".o")
         if force or _stale(src, obj, headers):
             extra = ["-Rpass-analysis=kernel-resource-usage"] if verbose_resource else []
-            _run([HIPCC, "-x", "hip", f"--offload-arch={ARCH}"] + COMMON + ["-Wno-unused-result", "-Wno-unused-value"]
-                 + extra + ["-c", src, "-o", obj])
+            _run([HIPCC, "-x", "hip", f"--offload-arch={ARCH}"] + COMMON + extra_d + ["-Wno-unused-result",
+                 "-Wno-unused-value"] + extra + ["-c", src, "-o", obj])
         objs.append(obj)
     if force or not os.path.exists(LIB) or any(os.path.getmtime(o) > os.path.getmtime(LIB) for o in objs):
         _run([HIPCC, "-shared", "-fPIC", "-o", LIB] + objs + ["-lz"])
@@ -57,4 +65,5 @@ def build(force=False, verbose_resource=False):
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv, verbose_resource="--resource" in sys.argv)
+    build(force="--force" in sys.argv, verbose_resource="--resource" in sys.argv,
+          defines=[a[2:] for a in sys.argv[1:] if a.startswith("-D")])

@@ -55,10 +55,14 @@ struct Bvh2 {
 };
 
 // SAH: the cost of visiting an inner node relative to testing one triangle (both builders, bit-identical trees)
+#ifndef RT_MAX_LEAF
+#define RT_MAX_LEAF 2  // BVH2 leaf size bound of both builders (leaves up to 2x this where the SAH prefers them);
+                       // 4 until round 4: C3 16-view batch 0.509 vs 0.475 ms/frame, C4 8.56 vs 8.05
+#endif
 #ifndef RT_SAH_TRAVERSAL
 #define RT_SAH_TRAVERSAL 0.5f
 #endif
-Bvh2 build_bvh2(const float* positions, int ntri, float eps, int max_leaf = 4);
+Bvh2 build_bvh2(const float* positions, int ntri, float eps, int max_leaf = RT_MAX_LEAF);
 
 // Wide BVH collapsed from a Bvh2 (greedy: open the child with the largest area until `width`
 // children, width <= 8; slots past `width` stay empty),

@@ -34,7 +34,7 @@ namespace rt {
 namespace gb {
 
 constexpr int NB = 32;          // SAH bins (bvh_build.cpp Bvh2Builder)
-constexpr int kMaxLeaf = 4;     // build_bvh2(..., max_leaf = 4)
+constexpr int kMaxLeaf = RT_MAX_LEAF;  // build_bvh2(..., max_leaf = RT_MAX_LEAF)
 constexpr int kMaxDepth = 36;   // bvh_build.cpp kMaxDepth (median splits past the guard)
 #ifndef RT_KSMALL
 #define RT_KSMALL 512

@@ -1198,6 +1198,8 @@ __device__ __forceinline__ void trav_node(const DevScene& S, Trav& T, int* stk, 
     typedef float f2 __attribute__((ext_vector_type(2)));
     const f2 b2x = {bx, bx}, b2y = {by, by}, b2z = {bz, bz}, a2x = {ax, ax}, a2y = {ay, ay}, a2z = {az, az};
     uint32_t hits = 0u, kbest = 0xFFFFFFFFu;
+    uint32_t keys[NW];
+    const uint32_t ni = __popc(imask);  // DIRECT: the inner children are slots 0 .. ni - 1 (slot_order)
 #pragma unroll
     for (int s = 0; s < NW; ++s) {
         const int wi = s >> 1, sh = (s & 1) * 16;
@@ -1214,7 +1216,18 @@ __device__ __forceinline__ void trav_node(const DevScene& S, Trav& T, int* stk, 
         const bool h = t0 <= t1;
         hits |= h ? (1u << s) : 0u;
         const uint32_t key = (__float_as_uint(t0) & ~7u) | (uint32_t)s;
-        kbest = (h && (mi & (1u << s))) ? min(kbest, key) : kbest;
+        if (DIRECT)
+            keys[s] = (h && (uint32_t)s < ni) ? key : 0xFFFFFFFFu;  // reduced by a min3 tree below
+        else
+            kbest = (h && (mi & (1u << s))) ? min(kbest, key) : kbest;
+    }
+    // the ray's direction along the node's sort axis (slot_order): a group's children are taken from the
+    // high slots first when it points back
+    const uint32_t back = DIRECT ? ((((uint32_t)sx | ((uint32_t)sy << 1) | ((uint32_t)sz << 2)) >> ((w3 >> 24) & 3u)) & 1u) : 0u;
+    if (DIRECT) {
+        static_assert(NW == 8, "the key tree assumes 8 slots");
+        kbest = min(min(min(keys[0], keys[1]), keys[2]), min(min(keys[3], keys[4]), keys[5]));
+        kbest = min(min(kbest, keys[6]), keys[7]);
     }
     hits &= m;
     T.lb = __float_as_uint(f1.y);
@@ -1227,12 +1240,11 @@ __device__ __forceinline__ void trav_node(const DevScene& S, Trav& T, int* stk, 
         cnt.rvj += __popc(ih);
     }
     if (ih) {
-        const uint32_t sbest = kbest & 7u;
+        const uint32_t sbest = kbest & 7u;  // nearest first (the axis order for the first child too: C3 batch
+                                             // 0.462 vs 0.458 ms/frame, 5.51 vs 5.35 node visits per ray)
         const uint32_t rest = ih & ~(1u << sbest);
         if (DIRECT) {
             if (rest) {
-                const uint32_t ax = (w3 >> 24) & 3u;
-                const uint32_t back = ax == 0u ? (uint32_t)sx : ax == 1u ? (uint32_t)sy : (uint32_t)sz;
                 stk[T.sp * RT_WAVE] = (int)((child_base << 9) | (back << 8) | rest);
                 ++T.sp;
             }

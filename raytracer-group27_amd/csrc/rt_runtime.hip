@@ -484,7 +484,7 @@ static int create_one(const rt_scene_desc* desc, int device, rt_ctx** out) {
         c->bvh2_depth = gbuild.bvh2_depth;
     } else {
         try {
-            const Bvh2 bvh = build_bvh2(desc->positions, ntri, eps, 4);
+            const Bvh2 bvh = build_bvh2(desc->positions, ntri, eps, RT_MAX_LEAF);
             bvh8 = build_bvh8(bvh, 8);
             c->bvh2_nodes = (int)bvh.nodes.size();
             c->bvh2_depth = bvh.max_depth;

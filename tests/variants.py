@@ -37,6 +37,7 @@ def all_variants(R):
         {R.OPT_KERNEL: df, R.OPT_OPAQUE: 1},                    # the opaque kernel's 4-wave (batch) build
         {R.OPT_KERNEL: df, R.OPT_OPAQUE: 2},                    # ... its 3-wave (single-frame) build
         {R.OPT_KERNEL: df, R.OPT_OPAQUE: 3},                    # ... its 4-wave build with the re-visit group stack
+        {R.OPT_KERNEL: df, R.OPT_OPAQUE: 4},                    # ... and with the first child in axis order
         {R.OPT_KERNEL: df, R.OPT_REFILL: 32},                   # ... and a half-wave refill
         {R.OPT_KERNEL: df, R.OPT_COOP: 1},                      # ... drain lane groups in the drain only
         {R.OPT_KERNEL: df, R.OPT_TREE: 0},                      # general kernels where the tree kernel is eligible

@@ -11,6 +11,10 @@ sys.path.insert(0, os.path.join(REPO, "raytracer-group27_amd"))
 import rt_amd as R  # noqa: E402
 
 args = sys.argv[1:]
+if "--lib" in args:  # another build of the library (A/B of builds)
+    i = args.index("--lib")
+    R.LIB_PATH = os.path.abspath(args[i + 1])
+    del args[i:i + 2]
 cfgs = [a for a in args if a.startswith("C") and ":" not in a] or ["C3"]
 variants = [(a.split(":", 1)[0], dict(x.split("=") for x in a.split(":", 1)[1].split(",") if x))
             for a in args if ":" in a] or [("default", {})]
