@@ -986,6 +986,8 @@ static bool use_df(const rt_ctx* c, const KParams& K) {
 // 3 (their tail is a few waves' serial chains, which run faster with more registers: 1.40-1.45 vs 1.56-1.63 ms)
 #define RT_OPAQUE_V (RT_V_W4 | RT_V_NOPF)
 #define RT_OPAQUE_V3 (RT_V_W3 | RT_V_NOPF)
+// single frames: the 3-wave build whose phases may end before every query is done (RT_V_ASYNC, P.refill)
+#define RT_OPAQUE_VF (RT_V_W3 | RT_V_NOPF | RT_V_ASYNC)
 
 // Renders that the opaque-scene kernel draws: pixels (not rt_shade's explicit rays) of a large scene
 // (the dynamic-fetch class) whose materials are all opaque, lit by point and spot lights only, without
@@ -996,9 +998,13 @@ static bool opaque_path(const rt_ctx* c, const KParams& K, bool pixels) {
     return pixels && c->opt_opaque != 0 && c->opt_variant < 0 && use_df(c, K) && K.S.all_opaque && K.S.nsl == 0 &&
            K.S.nplane == 0 && !K.S.tex_on && (K.glossy_n == 1 || !c->glossy_material);
 }
-// the opaque kernel's 3-wave build: single frames (RT_OPT_OPAQUE 1 / 2 force the 4- / 3-wave build)
-static bool opaque_w3(const rt_ctx* c, const KParams& K) {
-    return c->opt_opaque == 2 || (c->opt_opaque != 1 && c->opt_opaque != 3 && K.n_views <= 1);
+// the opaque kernel's build: view batches the 4-wave one, single frames the 3-wave one with partial refills
+// (RT_OPT_OPAQUE 1 / 2 force the 4-wave / the full-wave 3-wave build, 3 the 4-wave re-visit A/B)
+static int opaque_variant(const rt_ctx* c, const KParams& K) {
+    if (c->opt_opaque == 1) return RT_OPAQUE_V;
+    if (c->opt_opaque == 2) return RT_OPAQUE_V3;
+    if (c->opt_opaque == 3) return RT_OPAQUE_V | RT_V_REVISIT;
+    return K.n_views <= 1 ? RT_OPAQUE_VF : RT_OPAQUE_V;
 }
 
 // the recursion-tree kernel (rt_megakernel.hip persistent_tree_kernel): 4 / 3 waves per SIMD
@@ -1050,13 +1056,13 @@ static bool launch_shipped(bool df, int v, int grid, hipStream_t st, const KPara
 template <bool COUNT>
 static int launch_persistent(int grid, hipStream_t st, const KParams& K, const JobSrc& J, rt_ctx* c) {
     if (opaque_path(c, K, J.mode == 0)) {
-        const bool w3 = opaque_w3(c, K);
-        int v = w3 ? RT_OPAQUE_V3 : RT_OPAQUE_V;
-        if (c->opt_opaque == 3) {  // A/B: the 4-wave build with the re-visit group stack
-            v = RT_OPAQUE_V | RT_V_REVISIT;
+        const int v = opaque_variant(c, K);
+        if (v == (RT_OPAQUE_V | RT_V_REVISIT)) {  // A/B: the 4-wave build with the re-visit group stack
             hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V | RT_V_REVISIT>), dim3(grid), dim3(64), 0, st,
                                K, J);
-        } else if (w3) {
+        } else if (v == RT_OPAQUE_VF) {
+            hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_VF>), dim3(grid), dim3(64), 0, st, K, J);
+        } else if (v == RT_OPAQUE_V3) {
             hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V3>), dim3(grid), dim3(64), 0, st, K, J);
         } else {
             hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V>), dim3(grid), dim3(64), 0, st, K, J);
@@ -1104,12 +1110,13 @@ static int occupancy_of(int* per_cu) {
 // resident 64-lane blocks of the kernel (the persistent grid)
 static int persistent_grid(rt_ctx* c, const KParams& K, bool pixels) {
     if (opaque_path(c, K, pixels)) {
-        const int key = opaque_w3(c, K) ? 1 : 0;
+        const int v = opaque_variant(c, K);
+        const int key = (v & RT_V_W3) ? 1 : 0;  // 3 or 4 waves per SIMD
         if (c->opaque_blocks[key] > 0) return c->opaque_blocks[key];
         int cus = 0, per_cu = 0;
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
         const hipError_t e =
-            key ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V3>, 64, 0)
+            key ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_VF>, 64, 0)
                 : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V>, 64, 0);
         if (e != hipSuccess || per_cu <= 0) per_cu = 8;
         c->opaque_blocks[key] = std::max(1, cus) * per_cu;
