@@ -381,7 +381,7 @@ int rt_debug_counters(rt_ctx* ctx, uint64_t* out, int n);
 #define RT_OPT_FAN 7         /* dynamic-fetch kernel, opaque scenes: spherical-light samples as wave-shared fans (1, default) or per lane (0) */
 #define RT_OPT_DUAL_STEP 10  /* dynamic-fetch kernel: a lane testing leaf records also visits its next node in the same step (-1 default = 1, 0 off) */
 #define RT_OPT_CENTRE_FIRST 12 /* job order: the per-XCD tile ranges above the image centre walked bottom-up, so every range starts at its rows nearest the centre: -1 by render shape, 0 off, 1 on */
-#define RT_OPT_OPAQUE 11     /* opaque-scene kernel (opaque materials, point / spot lights, no lobes or textures): -1 where eligible (4 waves/SIMD for view batches, 3 for single frames), 0 never, 1 / 2 force the 4- / 3-wave build, 3 the 4-wave build with the re-visit group stack (A/B) */
+#define RT_OPT_OPAQUE 11     /* opaque-scene kernel (opaque materials, point / spot lights, no lobes or textures): -1 where eligible (the 4-wave build), 0 never, 1 the 4-wave build, 2 the 3-wave build, 3 the 4-wave build with the re-visit group stack (A/Bs) */
 #define RT_OPT_TREE 13       /* recursion-tree kernel (transparent materials, all four light types with <= 64-sample fans, no lobes or textures): -1 / 2 where eligible, 0 never, 1 its build with the re-visit group stack (A/B) */
 #define RT_OPT_PEER_STORES 14 /* split renders: -1 the replicas with peer access to devices[0] store their pixels straight into its images (default), 0 every replica renders band-dense on its own device and copies (the path of devices without peer access) */
 #define RT_KERNEL_AUTO 0

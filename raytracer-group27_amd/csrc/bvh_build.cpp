@@ -475,8 +475,8 @@ struct Bvh2Builder {
         const v3 ext = cb.hi - cb.lo;
         if (ext.y > ext.x) axis = 1;
         if (ext.z > (axis == 0 ? ext.x : ext.y)) axis = 2;
-        const float cmin = axis == 0 ? cb.lo.x : (axis == 1 ? cb.lo.y : cb.lo.z);
-        const float cext = axis == 0 ? ext.x : (axis == 1 ? ext.y : ext.z);
+        float cmin = axis == 0 ? cb.lo.x : (axis == 1 ? cb.lo.y : cb.lo.z);
+        float cext = axis == 0 ? ext.x : (axis == 1 ? ext.y : ext.z);
         auto cval = [&](int p) { return axis == 0 ? ce[p].x : (axis == 1 ? ce[p].y : ce[p].z); };
         int mid = -1;
         // depth guard: median splits halve the range, so switching to them once
@@ -487,6 +487,68 @@ struct Bvh2Builder {
         const bool sah_ok = depth + need < kMaxDepth;
         if (cext > 0.0f && sah_ok) {
             constexpr int NB = 32;
+            // RT_SAH_AXES 3: the binned SAH over every axis with centroid extent, the cheapest split wins (ties:
+            // the lower axis); 1: the axis of the largest centroid extent only (rt_build.hip does the same)
+            if (RT_SAH_AXES == 3) {
+                float best_all = FLT_MAX;
+                int best_axis = axis;
+                for (int a = 0; a < 3; ++a) {
+                    const float lo_a = a == 0 ? cb.lo.x : (a == 1 ? cb.lo.y : cb.lo.z);
+                    const float ext_a = a == 0 ? ext.x : (a == 1 ? ext.y : ext.z);
+                    if (!(ext_a > 0.0f)) continue;
+                    const float sc = NB / ext_a;
+                    Box ab[NB];
+                    int ac[NB] = {0};
+                    auto grow_bins = [&](int i0, int i1, Box* bx, int* cn) {
+                        for (int i = i0; i < i1; ++i) {
+                            const int p = ix[i];
+                            const float c = a == 0 ? ce[p].x : (a == 1 ? ce[p].y : ce[p].z);
+                            int b = (int)((c - lo_a) * sc);
+                            b = b < 0 ? 0 : (b >= NB ? NB - 1 : b);
+                            bx[b].grow(pb[p]);
+                            cn[b]++;
+                        }
+                    };
+                    if (par) {
+                        std::vector<std::array<Box, NB>> cbb(nch);
+                        std::vector<std::array<int, NB>> cbc(nch);
+                        parallel_for(nch, host_threads(), [&](int c) {
+                            cbc[c].fill(0);
+                            grow_bins(begin + c * kParChunk, std::min(end, begin + (c + 1) * kParChunk), cbb[c].data(),
+                                      cbc[c].data());
+                        });
+                        for (int c = 0; c < nch; ++c)
+                            for (int b = 0; b < NB; ++b) {
+                                ab[b].grow(cbb[c][b]);
+                                ac[b] += cbc[c][b];
+                            }
+                    } else {
+                        grow_bins(begin, end, ab, ac);
+                    }
+                    Box racc, lacc;
+                    float rar[NB];
+                    int rcn[NB], cnt = 0, lcnt = 0;
+                    for (int b = NB - 1; b > 0; --b) {
+                        racc.grow(ab[b]);
+                        cnt += ac[b];
+                        rar[b] = racc.area();
+                        rcn[b] = cnt;
+                    }
+                    for (int b = 1; b < NB; ++b) {
+                        lacc.grow(ab[b - 1]);
+                        lcnt += ac[b - 1];
+                        if (lcnt == 0 || rcn[b] == 0) continue;
+                        const float cost = lacc.area() * lcnt + rar[b] * rcn[b];
+                        if (cost < best_all) {
+                            best_all = cost;
+                            best_axis = a;
+                        }
+                    }
+                }
+                axis = best_axis;
+                cmin = axis == 0 ? cb.lo.x : (axis == 1 ? cb.lo.y : cb.lo.z);
+                cext = axis == 0 ? ext.x : (axis == 1 ? ext.y : ext.z);
+            }
             Box bb[NB];
             int bc[NB] = {0};
             const float scale = NB / cext;

@@ -992,8 +992,6 @@ __device__ __attribute__((noinline)) bool advance_lane_call(const void* ka, Lane
 
 #define RT_V_W3 8    // compiled for 3 waves per SIMD (168 VGPRs)
 #define RT_V_REVISIT 32  // opaque / tree kernels: the re-visit group stack of the other kernels (A/B), not DIRECT
-#define RT_V_ASYNC 64    // opaque kernel: a phase may end once P.refill lanes have finished their query (the others
-                         // keep tracing across the state machine); refill 64 = the full-wave phases
 #define RT_V_WAVES(V) (((V) & RT_V_W4) ? 4 : ((V) & RT_V_W3) ? 3 : 2)
 
 
@@ -2266,8 +2264,7 @@ __device__ __forceinline__ bool lite_advance(const KParams& P, LiteLane& L, bool
 
 template <bool COUNT, int V>
 __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KParams, JobSrc) {
-    constexpr bool PF = !(V & RT_V_NOPF), COOP = !(V & RT_V_NOCOOP), DIRECT = !(V & RT_V_REVISIT),
-                   ASYNC = (V & RT_V_ASYNC) != 0;
+    constexpr bool PF = !(V & RT_V_NOPF), COOP = !(V & RT_V_NOCOOP), DIRECT = !(V & RT_V_REVISIT);
     // the kernel's arguments are read where each phase uses them (fresh_kernarg), not held in SGPRs
     const void* ka = (const void*)__builtin_amdgcn_kernarg_segment_ptr();
 #define RT_FRESH const KParams& P = *(const KParams*)fresh_kernarg(ka); const DevScene& S = P.S
@@ -2353,15 +2350,10 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
         }
         if (COUNT) cnt.cyc_d += (unsigned long long)clock64() - tJ;
         // full-wave phases: no lane traces across phase A, so the traversal state is rebuilt for every lane
-        // here (a new query, or an empty walk) and nothing of it has to be kept across the state machine;
-        // ASYNC: lanes still tracing keep theirs
-        if (ASYNC) {
-            if (start) {
-                cnt.rays++;
-                trav_init_q(S, P.use_bvh != 0, q.o, q.d, q.t, L.shadow, qsdist, T);
-                tracing = true;
-            }
-        } else {
+        // here (a new query, or an empty walk) and nothing of it has to be kept across the state machine
+        // (phases that end once some queries are done, the others tracing on across the state machine:
+        // C3 frame 1.35-1.64 vs 1.25 ms at refill 32 / 16 / 8 / 2, profiles/r04/ab_r04g_refill.log)
+        {
             Trav Tn;
             if (start) {
                 cnt.rays++;
@@ -2403,9 +2395,8 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
                 pending = true;
             }
             // full-wave phases (refill 64, the batch and few-sample policy of the general kernel): the phase
-            // ends when no lane traces; ASYNC also once P.refill lanes wait for their state machine
+            // ends when no lane traces
             if (!__any(tracing)) break;
-            if (ASYNC && __popcll(__ballot(pending)) >= P.refill) break;
             if (COUNT && P.wave_trace && t_exh) {
                 it_drain++;
                 lanes_drain += (unsigned int)__popcll(__ballot(tracing));

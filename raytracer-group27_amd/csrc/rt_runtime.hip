@@ -133,7 +133,7 @@ struct rt_ctx {
     int opt_fan_cap = 0;      // pixels a wave may have waiting on fans before it stops taking new ones (0: default)
     int opt_dual = -1;        // dynamic-fetch steps: record and node visit in one iteration (-1 default, 0 off, 1 on)
     int opt_variant = -1;   // -1: the shipped variant for the render shape (RT_DF_BATCH / _FRAME, RT_WT_DEFAULT)
-    int opt_opaque = -1;    // opaque-scene kernel: -1 where eligible (build by render shape), 0 never, 1 / 2 the 4- / 3-wave build
+    int opt_opaque = -1;    // opaque-scene kernel: -1 where eligible (4-wave build), 0 never, 1 4-wave, 2 3-wave, 3 re-visit A/B
     int opt_tree = -1;      // recursion-tree kernel: -1 / 2 where eligible, 0 never, 1 its re-visit group stack build (A/B)
     char last_kernel[64] = {0};
     // view batches: the camera table's pinned host staging and the event of its last copy (the buffer
@@ -986,8 +986,6 @@ static bool use_df(const rt_ctx* c, const KParams& K) {
 // 3 (their tail is a few waves' serial chains, which run faster with more registers: 1.40-1.45 vs 1.56-1.63 ms)
 #define RT_OPAQUE_V (RT_V_W4 | RT_V_NOPF)
 #define RT_OPAQUE_V3 (RT_V_W3 | RT_V_NOPF)
-// single frames: the 3-wave build whose phases may end before every query is done (RT_V_ASYNC, P.refill)
-#define RT_OPAQUE_VF (RT_V_W3 | RT_V_NOPF | RT_V_ASYNC)
 
 // Renders that the opaque-scene kernel draws: pixels (not rt_shade's explicit rays) of a large scene
 // (the dynamic-fetch class) whose materials are all opaque, lit by point and spot lights only, without
@@ -998,13 +996,14 @@ static bool opaque_path(const rt_ctx* c, const KParams& K, bool pixels) {
     return pixels && c->opt_opaque != 0 && c->opt_variant < 0 && use_df(c, K) && K.S.all_opaque && K.S.nsl == 0 &&
            K.S.nplane == 0 && !K.S.tex_on && (K.glossy_n == 1 || !c->glossy_material);
 }
-// the opaque kernel's build: view batches the 4-wave one, single frames the 3-wave one with partial refills
-// (RT_OPT_OPAQUE 1 / 2 force the 4-wave / the full-wave 3-wave build, 3 the 4-wave re-visit A/B)
+// the opaque kernel's build: the 4-wave one for batches and single frames (round 4, with the direct group stack
+// and the leaf bound 2: C3 frame 1.237 vs 1.246 ms at 3 waves, profiles/r04/ab_r04g_refill.log; the 3-wave build
+// had won frames before); RT_OPT_OPAQUE 2 the 3-wave build, 3 the 4-wave re-visit A/B
 static int opaque_variant(const rt_ctx* c, const KParams& K) {
-    if (c->opt_opaque == 1) return RT_OPAQUE_V;
+    (void)K;
     if (c->opt_opaque == 2) return RT_OPAQUE_V3;
     if (c->opt_opaque == 3) return RT_OPAQUE_V | RT_V_REVISIT;
-    return K.n_views <= 1 ? RT_OPAQUE_VF : RT_OPAQUE_V;
+    return RT_OPAQUE_V;
 }
 
 // the recursion-tree kernel (rt_megakernel.hip persistent_tree_kernel): 4 / 3 waves per SIMD
@@ -1060,8 +1059,6 @@ static int launch_persistent(int grid, hipStream_t st, const KParams& K, const J
         if (v == (RT_OPAQUE_V | RT_V_REVISIT)) {  // A/B: the 4-wave build with the re-visit group stack
             hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V | RT_V_REVISIT>), dim3(grid), dim3(64), 0, st,
                                K, J);
-        } else if (v == RT_OPAQUE_VF) {
-            hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_VF>), dim3(grid), dim3(64), 0, st, K, J);
         } else if (v == RT_OPAQUE_V3) {
             hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V3>), dim3(grid), dim3(64), 0, st, K, J);
         } else {
@@ -1116,7 +1113,7 @@ static int persistent_grid(rt_ctx* c, const KParams& K, bool pixels) {
         int cus = 0, per_cu = 0;
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
         const hipError_t e =
-            key ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_VF>, 64, 0)
+            key ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V3>, 64, 0)
                 : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V>, 64, 0);
         if (e != hipSuccess || per_cu <= 0) per_cu = 8;
         c->opaque_blocks[key] = std::max(1, cus) * per_cu;

@@ -470,7 +470,7 @@ def test_opaque_kernel_spot_lights(R, O):
         ref, rays = O.Oracle(scene).render(prm, W, H)
         df = R.KERNEL_DYNAMIC_FETCH
         base = None
-        for opaque, refill in ((0, 0), (1, 0), (2, 0), (3, 0), (-1, 0), (-1, 1), (-1, 16)):
+        for opaque, refill in ((0, 0), (1, 0), (2, 0), (3, 0)):
             with V.options(R, ctx, {R.OPT_KERNEL: df, R.OPT_OPAQUE: opaque, R.OPT_REFILL: refill}):
                 img, st = ctx.render(cam, prm, W, H)
             assert ("opaque" in st.kernel_name) == (opaque != 0), (opaque, st.kernel_name)
