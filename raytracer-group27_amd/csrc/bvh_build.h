@@ -59,6 +59,9 @@ struct Bvh2 {
 #define RT_MAX_LEAF 2  // BVH2 leaf size bound of both builders (leaves up to 2x this where the SAH prefers them);
                        // 4 until round 4: C3 16-view batch 0.509 vs 0.475 ms/frame, C4 8.56 vs 8.05
 #endif
+#ifndef RT_SAH_AXES
+#define RT_SAH_AXES 3  // binned SAH over every axis (3) or the largest centroid extent only (1; until round 4)
+#endif
 #ifndef RT_SAH_TRAVERSAL
 #define RT_SAH_TRAVERSAL 0.5f
 #endif

@@ -42,6 +42,8 @@ constexpr int kMaxDepth = 36;   // bvh_build.cpp kMaxDepth (median splits past t
 constexpr int kSmall = RT_KSMALL;  // ranges up to this size are built as whole subtrees by one wave
 constexpr int kChunk = 4096;    // level-synchronous phase: triangles per workgroup
 constexpr int kBinW = 13;       // bin: count, box lo/hi, centroid lo/hi (ordered-uint min/max)
+constexpr int kAxes = RT_SAH_AXES;         // binned axes per range (bvh_build.h)
+constexpr int kTaskBins = kAxes * NB * kBinW;  // a range's bins: axis-major
 constexpr int kStack = 48;      // subtree wave: pending ranges
 
 // float <-> order-preserving uint (min/max by integer atomics)
@@ -294,6 +296,19 @@ __device__ __forceinline__ void bin_rule(const float* clo, const float* chi, int
     scale = cext > 0.0f ? (float)NB / cext : 0.0f;
 }
 
+// the bins of axis slot s (0 .. kAxes-1): every axis (kAxes 3), or the largest centroid extent's (kAxes 1)
+__device__ __forceinline__ void axis_rule(const float* clo, const float* chi, int s, int& axis, float& cmin,
+                                          float& cext, float& scale) {
+    if (kAxes == 1) {
+        bin_rule(clo, chi, axis, cmin, cext, scale);
+        return;
+    }
+    axis = s;
+    cmin = clo[s];
+    cext = chi[s] - clo[s];
+    scale = cext > 0.0f ? (float)NB / cext : 0.0f;
+}
+
 __device__ __forceinline__ int bin_of(float c, float cmin, float scale) {
     const int b = (int)((c - cmin) * scale);
     return b < 0 ? 0 : (b >= NB ? NB - 1 : b);
@@ -303,7 +318,7 @@ __device__ __forceinline__ float comp(const float4& v, int a) { return a == 0 ? 
 
 __global__ void k_init_bins(uint32_t* bins, int n) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n * NB * kBinW) return;
+    if (i >= n * kTaskBins) return;
     const int w = i % kBinW;
     bins[i] = w == 0 ? 0u : ((w == 1 || w == 2 || w == 3 || w == 7 || w == 8 || w == 9) ? 0xFFFFFFFFu : 0u);
 }
@@ -313,38 +328,40 @@ __global__ __launch_bounds__(256) void k_bin(const Chunk* __restrict__ chunks, c
                                              const int* __restrict__ idx, const float4* __restrict__ bmin,
                                              const float4* __restrict__ bmax, const float4* __restrict__ cent,
                                              uint32_t* bins) {
-    __shared__ uint32_t lb[NB * kBinW];
+    __shared__ uint32_t lb[kTaskBins];
     const Chunk ch = chunks[blockIdx.x];
     const LTask T = tasks[ch.task];
-    for (int i = threadIdx.x; i < NB * kBinW; i += blockDim.x) {
+    for (int i = threadIdx.x; i < kTaskBins; i += blockDim.x) {
         const int w = i % kBinW;
         lb[i] = w == 0 ? 0u : ((w >= 1 && w <= 3) || (w >= 7 && w <= 9) ? 0xFFFFFFFFu : 0u);
     }
     __syncthreads();
-    int axis;
-    float cmin, cext, scale;
-    bin_rule(T.clo, T.chi, axis, cmin, cext, scale);
-    for (int i = ch.begin + threadIdx.x; i < ch.end; i += blockDim.x) {
-        const int p = idx[i];
-        const float4 c = cent[p], lo = bmin[p], hi = bmax[p];
-        uint32_t* b = lb + bin_of(comp(c, axis), cmin, scale) * kBinW;
-        atomicAdd(b, 1u);
-        atomicMin(b + 1, f2o(lo.x));
-        atomicMin(b + 2, f2o(lo.y));
-        atomicMin(b + 3, f2o(lo.z));
-        atomicMax(b + 4, f2o(hi.x));
-        atomicMax(b + 5, f2o(hi.y));
-        atomicMax(b + 6, f2o(hi.z));
-        atomicMin(b + 7, f2o(c.x));
-        atomicMin(b + 8, f2o(c.y));
-        atomicMin(b + 9, f2o(c.z));
-        atomicMax(b + 10, f2o(c.x));
-        atomicMax(b + 11, f2o(c.y));
-        atomicMax(b + 12, f2o(c.z));
+    for (int s = 0; s < kAxes; ++s) {
+        int axis;
+        float cmin, cext, scale;
+        axis_rule(T.clo, T.chi, s, axis, cmin, cext, scale);
+        for (int i = ch.begin + threadIdx.x; i < ch.end; i += blockDim.x) {
+            const int p = idx[i];
+            const float4 c = cent[p], lo = bmin[p], hi = bmax[p];
+            uint32_t* b = lb + (s * NB + bin_of(comp(c, axis), cmin, scale)) * kBinW;
+            atomicAdd(b, 1u);
+            atomicMin(b + 1, f2o(lo.x));
+            atomicMin(b + 2, f2o(lo.y));
+            atomicMin(b + 3, f2o(lo.z));
+            atomicMax(b + 4, f2o(hi.x));
+            atomicMax(b + 5, f2o(hi.y));
+            atomicMax(b + 6, f2o(hi.z));
+            atomicMin(b + 7, f2o(c.x));
+            atomicMin(b + 8, f2o(c.y));
+            atomicMin(b + 9, f2o(c.z));
+            atomicMax(b + 10, f2o(c.x));
+            atomicMax(b + 11, f2o(c.y));
+            atomicMax(b + 12, f2o(c.z));
+        }
     }
     __syncthreads();
-    uint32_t* g = bins + (size_t)ch.task * NB * kBinW;
-    for (int i = threadIdx.x; i < NB * kBinW; i += blockDim.x) {
+    uint32_t* g = bins + (size_t)ch.task * kTaskBins;
+    for (int i = threadIdx.x; i < kTaskBins; i += blockDim.x) {
         const int w = i % kBinW;
         if (w == 0) {
             if (lb[i]) atomicAdd(g + i, lb[i]);
@@ -404,56 +421,68 @@ __global__ void k_split(const LTask* __restrict__ tasks, int ntask, const uint32
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= ntask) return;
     const LTask T = tasks[t];
-    const uint32_t* bn = bins + (size_t)t * NB * kBinW;
-    int axis;
-    float cmin, cext, scale;
-    bin_rule(T.clo, T.chi, axis, cmin, cext, scale);
-    Split sp{axis, -1, 0, 0, cmin, scale};
     const int n = T.end - T.begin;
     int need = 0;
     while ((kMaxLeaf << need) < n) ++need;
-    if (!(cext > 0.0f) || T.depth + need >= kMaxDepth) {
-        ctr->error = 1;  // degenerate centroids / depth guard on a large range: the host builds it
-        splits[t] = sp;
-        return;
-    }
-    float rarea[NB];
-    int rcnt[NB];
-    {
+    // the cheapest split over the binned axes (the first axis slot, then the first bin, on equal costs)
+    int axis = 0, best_b = -1, best_s = 0;
+    float cmin = 0.0f, scale = 0.0f, best = FLT_MAX;
+    bool any_ext = false;
+    for (int s = 0; s < kAxes; ++s) {
+        int ax;
+        float cm, ce, sc;
+        axis_rule(T.clo, T.chi, s, ax, cm, ce, sc);
+        if (!(ce > 0.0f)) continue;
+        any_ext = true;
+        const uint32_t* bs = bins + (size_t)t * kTaskBins + s * NB * kBinW;
+        float rarea[NB];
+        int rcnt[NB];
+        {
+            float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+            int cnt = 0;
+            for (int b = NB - 1; b > 0; --b) {
+                const uint32_t* x = bs + b * kBinW;
+                if (x[0]) {
+                    for (int a = 0; a < 3; ++a) {
+                        lo[a] = fminf(lo[a], o2f(x[1 + a]));
+                        hi[a] = fmaxf(hi[a], o2f(x[4 + a]));
+                    }
+                }
+                cnt += (int)x[0];
+                rarea[b] = box_area(lo, hi);
+                rcnt[b] = cnt;
+            }
+        }
         float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
-        int cnt = 0;
-        for (int b = NB - 1; b > 0; --b) {
-            const uint32_t* x = bn + b * kBinW;
+        int lcnt = 0;
+        for (int b = 1; b < NB; ++b) {
+            const uint32_t* x = bs + (b - 1) * kBinW;
             if (x[0]) {
                 for (int a = 0; a < 3; ++a) {
                     lo[a] = fminf(lo[a], o2f(x[1 + a]));
                     hi[a] = fmaxf(hi[a], o2f(x[4 + a]));
                 }
             }
-            cnt += (int)x[0];
-            rarea[b] = box_area(lo, hi);
-            rcnt[b] = cnt;
-        }
-    }
-    float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
-    int lcnt = 0, best_b = -1;
-    float best = FLT_MAX;
-    for (int b = 1; b < NB; ++b) {
-        const uint32_t* x = bn + (b - 1) * kBinW;
-        if (x[0]) {
-            for (int a = 0; a < 3; ++a) {
-                lo[a] = fminf(lo[a], o2f(x[1 + a]));
-                hi[a] = fmaxf(hi[a], o2f(x[4 + a]));
+            lcnt += (int)x[0];
+            if (lcnt == 0 || rcnt[b] == 0) continue;
+            const float cost = box_area(lo, hi) * lcnt + rarea[b] * rcnt[b];
+            if (cost < best) {
+                best = cost;
+                best_b = b;
+                best_s = s;
+                axis = ax;
+                cmin = cm;
+                scale = sc;
             }
         }
-        lcnt += (int)x[0];
-        if (lcnt == 0 || rcnt[b] == 0) continue;
-        const float cost = box_area(lo, hi) * lcnt + rarea[b] * rcnt[b];
-        if (cost < best) {
-            best = cost;
-            best_b = b;
-        }
     }
+    Split sp{axis, -1, 0, 0, cmin, scale};
+    if (!any_ext || T.depth + need >= kMaxDepth) {
+        ctr->error = 1;  // degenerate centroids / depth guard on a large range: the host builds it
+        splits[t] = sp;
+        return;
+    }
+    const uint32_t* bn = bins + (size_t)t * kTaskBins + best_s * NB * kBinW;  // the chosen axis's bins
     if (best_b <= 0) {
         ctr->error = 1;
         splits[t] = sp;
@@ -651,7 +680,7 @@ __device__ __forceinline__ void wave_box(const int* idx, int b, int e, const flo
 __global__ __launch_bounds__(256) void k_subtrees(const STask* __restrict__ tasks, int ntask, int* idx, int* idx2,
                                                   const float4* __restrict__ bmin, const float4* __restrict__ bmax,
                                                   const float4* __restrict__ cent, Bvh2Node* nodes, Ctrs* ctr) {
-    __shared__ uint32_t bins_s[4][NB * kBinW];
+    __shared__ uint32_t bins_s[4][kTaskBins];
     __shared__ SEntry stack_s[4][kStack];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int t = blockIdx.x * 4 + w;
@@ -685,72 +714,97 @@ __global__ __launch_bounds__(256) void k_subtrees(const STask* __restrict__ task
         wave_sync();
         const int n = E.end - E.begin;
         maxd = max(maxd, E.depth);
-        int axis;
-        float cmin, cext, scale;
-        bin_rule(E.clo, E.chi, axis, cmin, cext, scale);
+        int axis = 0;
+        float cmin = 0.0f, scale = 0.0f;
+        bool any_ext = false;
+        for (int s = 0; s < kAxes; ++s) {
+            int ax;
+            float cm, ce, sc;
+            axis_rule(E.clo, E.chi, s, ax, cm, ce, sc);
+            any_ext = any_ext || ce > 0.0f;
+        }
         int need = 0;
         while ((kMaxLeaf << need) < n) ++need;
         const bool sah_ok = E.depth + need < kMaxDepth;
         int mid = -1, best_b = -1;
         bool make_leaf = false;
-        if (cext > 0.0f && sah_ok) {
-            for (int i = lane; i < NB * kBinW; i += 64) {
+        if (any_ext && sah_ok) {
+            for (int i = lane; i < kTaskBins; i += 64) {
                 const int k = i % kBinW;
                 bins[i] = k == 0 ? 0u : ((k >= 1 && k <= 3) || (k >= 7 && k <= 9) ? 0xFFFFFFFFu : 0u);
             }
             wave_sync();
-            for (int i = E.begin + lane; i < E.end; i += 64) {
-                const int p = idx[i];
-                const float4 c = cent[p], lo = bmin[p], hi = bmax[p];
-                uint32_t* b = bins + bin_of(comp(c, axis), cmin, scale) * kBinW;
-                atomicAdd(b, 1u);
-                atomicMin(b + 1, f2o(lo.x));
-                atomicMin(b + 2, f2o(lo.y));
-                atomicMin(b + 3, f2o(lo.z));
-                atomicMax(b + 4, f2o(hi.x));
-                atomicMax(b + 5, f2o(hi.y));
-                atomicMax(b + 6, f2o(hi.z));
-                atomicMin(b + 7, f2o(c.x));
-                atomicMin(b + 8, f2o(c.y));
-                atomicMin(b + 9, f2o(c.z));
-                atomicMax(b + 10, f2o(c.x));
-                atomicMax(b + 11, f2o(c.y));
-                atomicMax(b + 12, f2o(c.z));
+            for (int s = 0; s < kAxes; ++s) {
+                int ax;
+                float cm, ce, sc;
+                axis_rule(E.clo, E.chi, s, ax, cm, ce, sc);
+                for (int i = E.begin + lane; i < E.end; i += 64) {
+                    const int p = idx[i];
+                    const float4 c = cent[p], lo = bmin[p], hi = bmax[p];
+                    uint32_t* b = bins + (s * NB + bin_of(comp(c, ax), cm, sc)) * kBinW;
+                    atomicAdd(b, 1u);
+                    atomicMin(b + 1, f2o(lo.x));
+                    atomicMin(b + 2, f2o(lo.y));
+                    atomicMin(b + 3, f2o(lo.z));
+                    atomicMax(b + 4, f2o(hi.x));
+                    atomicMax(b + 5, f2o(hi.y));
+                    atomicMax(b + 6, f2o(hi.z));
+                    atomicMin(b + 7, f2o(c.x));
+                    atomicMin(b + 8, f2o(c.y));
+                    atomicMin(b + 9, f2o(c.z));
+                    atomicMax(b + 10, f2o(c.x));
+                    atomicMax(b + 11, f2o(c.y));
+                    atomicMax(b + 12, f2o(c.z));
+                }
             }
             wave_sync();
-            // lane b (1..31): the cost of splitting before bin b (Bvh2Builder's sweeps, per lane)
-            float cost = FLT_MAX;
-            if (lane >= 1 && lane < NB) {
-                float llo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, lhi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
-                float rlo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, rhi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
-                int nl = 0, nr = 0;
-                for (int b = 0; b < NB; ++b) {
-                    const uint32_t* x = bins + b * kBinW;
-                    if (!x[0]) continue;
-                    float* lo = b < lane ? llo : rlo;
-                    float* hi = b < lane ? lhi : rhi;
-                    for (int a = 0; a < 3; ++a) {
-                        lo[a] = fminf(lo[a], o2f(x[1 + a]));
-                        hi[a] = fmaxf(hi[a], o2f(x[4 + a]));
+            // lane b (1..31), per axis slot: the cost of splitting before bin b (Bvh2Builder's sweeps, per
+            // lane); the key orders (cost, axis slot, bin): the first axis, then the first bin, on equal costs
+            unsigned long long key = ~0ull;
+            for (int s = 0; s < kAxes; ++s) {
+                int ax;
+                float cm, ce, sc;
+                axis_rule(E.clo, E.chi, s, ax, cm, ce, sc);
+                float cost = FLT_MAX;
+                if (ce > 0.0f && lane >= 1 && lane < NB) {
+                    const uint32_t* bs = bins + s * NB * kBinW;
+                    float llo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, lhi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+                    float rlo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, rhi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+                    int nl = 0, nr = 0;
+                    for (int b = 0; b < NB; ++b) {
+                        const uint32_t* x = bs + b * kBinW;
+                        if (!x[0]) continue;
+                        float* lo = b < lane ? llo : rlo;
+                        float* hi = b < lane ? lhi : rhi;
+                        for (int a = 0; a < 3; ++a) {
+                            lo[a] = fminf(lo[a], o2f(x[1 + a]));
+                            hi[a] = fmaxf(hi[a], o2f(x[4 + a]));
+                        }
+                        (b < lane ? nl : nr) += (int)x[0];
                     }
-                    (b < lane ? nl : nr) += (int)x[0];
+                    if (nl > 0 && nr > 0) cost = box_area(llo, lhi) * nl + box_area(rlo, rhi) * nr;
                 }
-                if (nl > 0 && nr > 0) cost = box_area(llo, lhi) * nl + box_area(rlo, rhi) * nr;
+                const unsigned long long k = ((unsigned long long)__float_as_uint(cost) << 32) | (unsigned)(s * 64 + lane);
+                key = k < key ? k : key;
             }
-            // the first bin with the smallest cost (strict < in the host's sweep)
-            unsigned long long key = ((unsigned long long)__float_as_uint(cost) << 32) | (unsigned)lane;
             for (int o = 32; o > 0; o >>= 1) {
                 const unsigned long long k2 = __shfl_xor(key, o);
                 key = k2 < key ? k2 : key;
             }
             const float best = __uint_as_float((uint32_t)(key >> 32));
             best_b = best < FLT_MAX ? (int)(key & 63ull) : -1;
+            const int best_s = best < FLT_MAX ? (int)((key >> 6) & 3ull) : 0;
+            {
+                float ce;
+                axis_rule(E.clo, E.chi, best_s, axis, cmin, ce, scale);
+            }
+            const uint32_t* bs = bins + best_s * NB * kBinW;
             const float leaf_cost = box_area(E.lo, E.hi) * n;
             const float split_cost = RT_SAH_TRAVERSAL * box_area(E.lo, E.hi) + best;
             if (best_b > 0 && (split_cost < leaf_cost || n > 2 * kMaxLeaf)) {
                 // stable partition into idx2, then back
                 int nl = 0;
-                for (int b = 0; b < best_b; ++b) nl += (int)bins[b * kBinW];
+                for (int b = 0; b < best_b; ++b) nl += (int)bs[b * kBinW];
                 int bl = E.begin, br = E.begin + nl;
                 for (int i0 = E.begin; i0 < E.end; i0 += 64) {
                     const int i = i0 + lane;
@@ -1255,7 +1309,7 @@ bool gpu_build(const float* h_pos, int ntri, const float* sph4, int nsph, GpuBui
     LTask *lt = B.get<LTask>(max_tasks), *lt_next = B.get<LTask>(max_tasks);
     STask* small = B.get<STask>(max_small);
     Split* splits = B.get<Split>(max_tasks);
-    uint32_t* bins = B.get<uint32_t>((size_t)max_tasks * NB * kBinW);
+    uint32_t* bins = B.get<uint32_t>((size_t)max_tasks * kTaskBins);
     const int max_chunks = ntri / kChunk + max_tasks + 16;
     Chunk* d_chunks = B.get<Chunk>(max_chunks);
     int* nleft = B.get<int>(max_chunks);
@@ -1282,7 +1336,7 @@ bool gpu_build(const float* h_pos, int ntri, const float* sph4, int nsph, GpuBui
         for (int b = 0; b < ntri; b += kChunk) chunks.push_back(Chunk{0, b, std::min(ntri, b + kChunk), 0});
         GB_CHECK(hipMemcpy(lt, &r, sizeof(LTask), hipMemcpyHostToDevice));
         GB_CHECK(hipMemcpy(d_chunks, chunks.data(), chunks.size() * sizeof(Chunk), hipMemcpyHostToDevice));
-        k_init_bins<<<grid(NB * kBinW, 256), 256, 0, st>>>(bins, 1);
+        k_init_bins<<<grid(kTaskBins, 256), 256, 0, st>>>(bins, 1);
         k_bin<<<(int)chunks.size(), 256, 0, st>>>(d_chunks, lt, idx, bmin, bmax, cent, bins);
         std::vector<uint32_t> hb(NB * kBinW);
         GB_CHECK(hipMemcpyAsync(hb.data(), bins, hb.size() * 4, hipMemcpyDeviceToHost, st));
@@ -1320,7 +1374,7 @@ bool gpu_build(const float* h_pos, int ntri, const float* sph4, int nsph, GpuBui
         const int nc = (int)chunks.size();
         GB_CHECK(hipMemcpy(d_chunks, chunks.data(), nc * sizeof(Chunk), hipMemcpyHostToDevice));
         GB_CHECK(hipMemsetAsync(&ctr->nlarge, 0, sizeof(int), st));
-        k_init_bins<<<grid((long long)nlevel * NB * kBinW, 256), 256, 0, st>>>(bins, nlevel);
+        k_init_bins<<<grid((long long)nlevel * kTaskBins, 256), 256, 0, st>>>(bins, nlevel);
         k_bin<<<nc, 256, 0, st>>>(d_chunks, lt, idx, bmin, bmax, cent, bins);
         k_split<<<grid(nlevel, 64), 64, 0, st>>>(lt, nlevel, bins, splits, nodes2, lt_next, max_tasks, small, max_small,
                                                  ctr);
