@@ -788,7 +788,7 @@ static void children_of(const Bvh2& b2, int node, std::vector<Child2>& out) {
 
 static float decode(float origin, int e, uint32_t q) {
     const float scale = std::ldexp(1.0f, e);
-    return origin + (float)q * scale;  // same two IEEE ops as the device decode
+    return origin + plane_q(q) * scale;  // same two IEEE ops as the device decode
 }
 }  // namespace
 
@@ -874,17 +874,16 @@ Bvh8 build_bvh8(const Bvh2& b2, int width) {
                 uint32_t imask = 0, lmask = 0, counts = 0;
                 uint16_t q[6][8];
                 for (int sl = 0; sl < 8; ++sl)
-                    for (int k = 0; k < 6; ++k) q[k][sl] = (k < 3) ? 65535 : 0;  // empty: inverted box
+                    for (int k = 0; k < 6; ++k) q[k][sl] = (k < 3) ? plane_max() : 0;  // empty: inverted box
                 for (size_t sl = 0; sl < ch.size(); ++sl) {
                     const Child2& c = ch[sl];
                     for (int a = 0; a < 3; ++a) {
                         const float scale = std::ldexp(1.0f, e[a]);
-                        long ql = (long)std::floor(((double)c.lo[a] - (double)lo[a]) / scale);
-                        long qh = (long)std::ceil(((double)c.hi[a] - (double)lo[a]) / scale);
-                        ql = std::max(0L, std::min(65535L, ql));
-                        qh = std::max(0L, std::min(65535L, qh));
+                        long ql = (long)plane_down(((double)c.lo[a] - (double)lo[a]) / scale);
+                        long qh = (long)plane_up(((double)c.hi[a] - (double)lo[a]) / scale);
+                        const long qmax = (long)plane_max();
                         while (ql > 0 && decode(lo[a], e[a], (uint32_t)ql) > c.lo[a]) --ql;
-                        while (qh < 65535 && decode(lo[a], e[a], (uint32_t)qh) < c.hi[a]) ++qh;
+                        while (qh < qmax && decode(lo[a], e[a], (uint32_t)qh) < c.hi[a]) ++qh;
                         if (decode(lo[a], e[a], (uint32_t)ql) > c.lo[a] || decode(lo[a], e[a], (uint32_t)qh) < c.hi[a])
                             err[j] = "BVH8 quantisation is not conservative";
                         q[a][sl] = (uint16_t)ql;

@@ -88,6 +88,44 @@ Bvh8 build_bvh8(const Bvh2& b2, int width = 8);
 // f(begin, end) over [0, n) in chunks of `chunk`, on the host's threads (scene upload loops)
 void parallel_chunks(int n, int chunk, const std::function<void(int, int)>& f);
 
+#ifndef RT_PLANES_F16
+#define RT_PLANES_F16 1  // BVH8 child planes: IEEE half offsets (1) or 16-bit integers (0; until round 4)
+#endif
+
+// BVH8 child planes (both builders, every traversal): a plane of axis a is origin[a] + q * 2^e[a] with q a 16-bit
+// word -- an IEEE binary16 value (RT_PLANES_F16: the traversal's slab distance is one v_fma_mix_f32 per plane,
+// the half widened inside the fma) or an unsigned integer.  plane_q is q's value; plane_max the largest word.
+RT_HD float plane_q(uint32_t q) {
+    if (!RT_PLANES_F16) return (float)q;
+    const uint32_t m = q & 0x3FFu, ex = (q >> 10) & 0x1Fu;  // non-negative finite halves only (q <= 0x7BFF)
+    return ex == 0 ? (float)m * 5.9604644775390625e-08f : ldexpf(1.0f + (float)m * 0.0009765625f, (int)ex - 15);
+}
+RT_HD uint32_t plane_max() { return RT_PLANES_F16 ? 0x7BFFu : 65535u; }
+// the largest word whose value is <= x (x >= 0), and the smallest whose value is >= x: the conservative rounding
+// of a child's lo / hi plane (values grow with the word, so a binary search over the words)
+RT_HD uint32_t plane_down(double x) {
+    uint32_t lo = 0, hi = plane_max();
+    if (!(x > 0.0)) return 0;
+    if ((double)plane_q(hi) <= x) return hi;
+    while (lo < hi) {  // invariant: value(lo) <= x < value(hi + 1)
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if ((double)plane_q(mid) <= x) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+RT_HD uint32_t plane_up(double x) {
+    uint32_t lo = 0, hi = plane_max();
+    if (!(x > 0.0)) return 0;
+    if ((double)plane_q(hi) < x) return hi;
+    while (lo < hi) {  // the first word with value >= x
+        const uint32_t mid = (lo + hi) >> 1;
+        if ((double)plane_q(mid) >= x) hi = mid;
+        else lo = mid + 1;
+    }
+    return lo;
+}
+
 // BVH8 slot order, one rule for both builders (bvh_build.cpp build_bvh8, rt_build.hip k_collapse): the
 // inner children first, sorted by the centre of their boxes (lo + hi) along the node's longest axis
 // (stable), then the leaves in collapse order.  With the inner children in the low slots a child's node

@@ -920,7 +920,7 @@ __device__ __forceinline__ int children_of(const Bvh2Node* nodes, int node, Chil
 
 __device__ __forceinline__ float decode_q(float origin, int e, uint32_t q) {
     const float scale = ldexpf(1.0f, e);
-    return origin + (float)q * scale;
+    return origin + plane_q(q) * scale;
 }
 
 __global__ void k_collapse(const Item8* __restrict__ items, int m, const Bvh2Node* __restrict__ nodes2,
@@ -975,18 +975,17 @@ __global__ void k_collapse(const Item8* __restrict__ items, int m, const Bvh2Nod
     uint32_t imask = 0, lmask = 0, cnts = 0;
     uint32_t q[6][8];
     for (int sl = 0; sl < 8; ++sl)
-        for (int k = 0; k < 6; ++k) q[k][sl] = (k < 3) ? 65535u : 0u;
+        for (int k = 0; k < 6; ++k) q[k][sl] = (k < 3) ? plane_max() : 0u;
     int n_inner = 0, n_rec = 0;
     for (int sl = 0; sl < nch; ++sl) {
         const Child2& c = ch[sl];
         for (int a = 0; a < 3; ++a) {
             const float scale = ldexpf(1.0f, e[a]);
-            long long ql = (long long)floor(((double)c.lo[a] - (double)lo[a]) / scale);
-            long long qh = (long long)ceil(((double)c.hi[a] - (double)lo[a]) / scale);
-            ql = ql < 0 ? 0 : (ql > 65535 ? 65535 : ql);
-            qh = qh < 0 ? 0 : (qh > 65535 ? 65535 : qh);
+            long long ql = (long long)plane_down(((double)c.lo[a] - (double)lo[a]) / scale);
+            long long qh = (long long)plane_up(((double)c.hi[a] - (double)lo[a]) / scale);
+            const long long qmax = (long long)plane_max();
             while (ql > 0 && decode_q(lo[a], e[a], (uint32_t)ql) > c.lo[a]) --ql;
-            while (qh < 65535 && decode_q(lo[a], e[a], (uint32_t)qh) < c.hi[a]) ++qh;
+            while (qh < qmax && decode_q(lo[a], e[a], (uint32_t)qh) < c.hi[a]) ++qh;
             if (decode_q(lo[a], e[a], (uint32_t)ql) > c.lo[a] || decode_q(lo[a], e[a], (uint32_t)qh) < c.hi[a])
                 atomicOr(err, 8);
             q[a][sl] = (uint32_t)ql;

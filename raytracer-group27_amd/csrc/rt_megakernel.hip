@@ -151,6 +151,14 @@ __device__ __forceinline__ bool test_records(const DevScene& S, int first, int c
 
 __device__ __forceinline__ float pow2f(uint32_t biased) { return __int_as_float((int)(biased << 23)); }
 
+// the value of the 16-bit child plane word at bit sh of w (bvh_build.h plane_q): a binary16 widened exactly
+// (RT_PLANES_F16; used as an fma operand the widening folds into v_fma_mix_f32) or an unsigned integer
+__device__ __forceinline__ float plane_f(uint32_t w, int sh) {
+    const unsigned short h = (unsigned short)((w >> sh) & 0xFFFFu);
+    if constexpr (RT_PLANES_F16) return (float)__builtin_bit_cast(_Float16, h);
+    else return (float)h;
+}
+
 template <bool COUNT, int NW>
 __device__ __forceinline__ bool trace_query8(const DevScene& S, v3 o, v3 d, float t_init, float thr, bool REF,
                                              bool ANY, Best& best, int* stk, Cnt& cnt) {
@@ -204,7 +212,7 @@ __device__ __forceinline__ bool trace_query8(const DevScene& S, v3 o, v3 d, floa
                     const int wi = s >> 1, sh = (s & 1) * 16;
                     auto q = [&](const float4& f) {
                         const uint32_t wv = __float_as_uint(wi == 0 ? f.x : wi == 1 ? f.y : wi == 2 ? f.z : f.w);
-                        return (float)((wv >> sh) & 0xFFFFu);
+                        return plane_f(wv, sh);
                     };
                     const float tlx = fmaf(q(qlx), bx, ax), thx = fmaf(q(qhx), bx, ax);
                     const float tly = fmaf(q(qly), by, ay), thy = fmaf(q(qhy), by, ay);
@@ -1203,14 +1211,17 @@ __device__ __forceinline__ void trav_node(const DevScene& S, Trav& T, int* stk, 
 #pragma unroll
     for (int s = 0; s < NW; ++s) {
         const int wi = s >> 1, sh = (s & 1) * 16;
-        auto q = [&](const float4& n, const float4& f) {
-            const uint32_t wn = __float_as_uint(wi == 0 ? n.x : wi == 1 ? n.y : wi == 2 ? n.z : n.w);
-            const uint32_t wf = __float_as_uint(wi == 0 ? f.x : wi == 1 ? f.y : wi == 2 ? f.z : f.w);
-            return f2{(float)((wn >> sh) & 0xFFFFu), (float)((wf >> sh) & 0xFFFFu)};
-        };
-        const f2 tx = __builtin_elementwise_fma(q(nx, fx), b2x, a2x);  // (near, far)
-        const f2 ty = __builtin_elementwise_fma(q(ny, fy), b2y, a2y);
-        const f2 tz = __builtin_elementwise_fma(q(nz, fz), b2z, a2z);
+        auto w = [&](const float4& v) { return __float_as_uint(wi == 0 ? v.x : wi == 1 ? v.y : wi == 2 ? v.z : v.w); };
+        f2 tx, ty, tz;  // (near, far)
+        if constexpr (RT_PLANES_F16) {  // one v_fma_mix_f32 per plane (the half widened inside the fma)
+            tx = f2{fmaf(plane_f(w(nx), sh), bx, ax), fmaf(plane_f(w(fx), sh), bx, ax)};
+            ty = f2{fmaf(plane_f(w(ny), sh), by, ay), fmaf(plane_f(w(fy), sh), by, ay)};
+            tz = f2{fmaf(plane_f(w(nz), sh), bz, az), fmaf(plane_f(w(fz), sh), bz, az)};
+        } else {  // integer planes: converted, then near and far in one packed fma
+            tx = __builtin_elementwise_fma(f2{plane_f(w(nx), sh), plane_f(w(fx), sh)}, b2x, a2x);
+            ty = __builtin_elementwise_fma(f2{plane_f(w(ny), sh), plane_f(w(fy), sh)}, b2y, a2y);
+            tz = __builtin_elementwise_fma(f2{plane_f(w(nz), sh), plane_f(w(fz), sh)}, b2z, a2z);
+        }
         const float t0 = fmaxf(fmaxf(tx.x, ty.x), fmaxf(tz.x, 0.0f));
         const float t1 = fminf(fminf(tx.y, ty.y), fminf(tz.y, tcull));
         const bool h = t0 <= t1;
@@ -1420,7 +1431,7 @@ __device__ __forceinline__ void node_slot_hits(const float4* np, v3 o, v3 inv, f
             const int wi = s >> 1, sh = (s & 1) * 16;
             auto q = [&](const float4& f) {
                 const uint32_t wv = __float_as_uint(wi == 0 ? f.x : wi == 1 ? f.y : wi == 2 ? f.z : f.w);
-                return (float)((wv >> sh) & 0xFFFFu);
+                return plane_f(wv, sh);
             };
             const float tlx = fmaf(q(qlx), bx, ax), thx = fmaf(q(qhx), bx, ax);
             const float tly = fmaf(q(qly), by, ay), thy = fmaf(q(qhy), by, ay);
