@@ -377,7 +377,7 @@ int rt_debug_counters(rt_ctx* ctx, uint64_t* out, int n);
 #define RT_OPT_WAVE_TRACE 5  /* 1: record rt_debug_wave_trace data */
 #define RT_OPT_VARIANT 6     /* developer A/B: compiled kernel variant (rt_megakernel.hip RT_V_*), -1 default */
 #define RT_OPT_FAN_CAP 9     /* fan renders: pixels a wave may have waiting on fans before it takes no new ones (0: default 16) */
-#define RT_OPT_INTERLEAVE 8  /* job -> pixel order: -1 by render shape, 0 8x8 tiles per wave, 1 one pixel of each of 64 tiles per wave */
+#define RT_OPT_INTERLEAVE 8  /* job -> pixel order: -1 by render shape, 0 8x8 tiles per wave, 1 one pixel of each of 64 tiles per wave, k = 2..5 64 / 2^k pixels of each of 2^k tiles */
 #define RT_OPT_FAN 7         /* dynamic-fetch kernel, opaque scenes: spherical-light samples as wave-shared fans (1, default) or per lane (0) */
 #define RT_OPT_DUAL_STEP 10  /* dynamic-fetch kernel: a lane testing leaf records also visits its next node in the same step (-1 default = 1, 0 off) */
 #define RT_OPT_CENTRE_FIRST 12 /* job order: the per-XCD tile ranges above the image centre walked bottom-up, so every range starts at its rows nearest the centre: -1 by render shape, 0 off, 1 on */

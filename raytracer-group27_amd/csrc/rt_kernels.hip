@@ -102,7 +102,7 @@ struct KParams {
     int refill;                 // dynamic-fetch kernel: waiting lanes that end a traversal phase
     int shade_level;            // rt_shade: recursion level of the explicit rays (getFinalColor's `level`)
     int fan;                    // dynamic-fetch kernel: bit 0 spherical-, bit 1 plane-light samples as wave-shared fans
-    int interleave;             // job -> pixel: a wave's 64 jobs are one pixel of each of 64 tiles
+    int interleave;             // job -> pixel: 0 a wave's 64 jobs are one 8x8 tile; k > 0 they spread over 2^k tiles
     int centre_first;           // job -> tile: the upper half's per-XCD tile ranges walked bottom-up (single frames)
     int fan_cap;                // ... a wave with this many pixels waiting on fans takes no new pixels
     int dual;                   // dynamic-fetch kernel: a lane testing a leaf's records also visits its next node

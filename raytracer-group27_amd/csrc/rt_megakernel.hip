@@ -817,11 +817,12 @@ __device__ __forceinline__ bool job_pixel(const KParams& P, int gjob, uint32_t& 
     int view;
     int job = view_job(P, gjob, view);
     if (P.interleave) {
-        // blocks of 64 tiles: the block's r-th job is pixel r / nb of its tile r % nb, so the 64
-        // jobs one wave takes lie in 64 tiles, and an expensive patch of the image is shared by
-        // many waves instead of held by one
-        const int nt = P.view_jobs >> 6, b = job >> 12, nb = min(64, nt - (b << 6)), r = job & 4095;
-        job = (((b << 6) + r % nb) << 6) + r / nb;
+        // groups of k = 2^interleave tiles: the group's r-th job is pixel r / nb of its tile r % nb, so the
+        // 64 jobs one wave takes lie in k tiles (64 / k pixels of each), and an expensive patch of the image
+        // is shared by k waves instead of held by one
+        const int kl = P.interleave, nt = P.view_jobs >> 6, b = job >> (6 + kl);
+        const int nb = min(1 << kl, nt - (b << kl)), r = job & ((64 << kl) - 1);
+        job = (((b << kl) + r % nb) << 6) + r / nb;
     }
     const int tiles_x = (P.W + 7) / 8;
     const int tiles_y_band = (P.band_rows + 7) / 8;

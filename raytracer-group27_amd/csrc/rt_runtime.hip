@@ -128,7 +128,7 @@ struct rt_ctx {
     int opt_refill = 0;     // 0: per render shape
     int opt_wave_trace = 0;
     int opt_fan = 1;        // dynamic-fetch kernel: spherical-light samples as wave-shared fans
-    int opt_interleave = -1;  // job -> pixel interleave: -1 by render shape, 0 off, 1 on
+    int opt_interleave = -1;  // job -> pixel interleave: -1 by render shape, 0 off, 1 over 64 tiles, 2..6 over 2^k
     int opt_centre_first = -1;  // job -> tile: upper ranges bottom-up: -1 by render shape, 0 off, 1 on
     int opt_fan_cap = 0;      // pixels a wave may have waiting on fans before it stops taking new ones (0: default)
     int opt_dual = -1;        // dynamic-fetch steps: record and node visit in one iteration (-1 default, 0 off, 1 on)
@@ -899,7 +899,7 @@ static int set_option_one(rt_ctx* c, int option, int value) {
             c->opt_fan_cap = value;
             return RT_OK;
         case RT_OPT_INTERLEAVE:
-            if (value < -1 || value > 1) break;
+            if (value < -1 || value > 6) break;
             c->opt_interleave = value;
             return RT_OK;
         case RT_OPT_CENTRE_FIRST:
@@ -1290,7 +1290,12 @@ static void shape_options(const rt_ctx* c, KParams& K) {
     K.fan_cap = c->opt_fan_cap > 0 ? c->opt_fan_cap : 16;
     // single frames with fans: a wave's jobs spread over 64 tiles (C4 52.9 -> 31.4 ms; the tile order
     // keeps its coherence elsewhere: C3 2.18 vs 2.41 ms, C2 0.77 vs 0.98 ms)
-    K.interleave = c->opt_interleave >= 0 ? c->opt_interleave : (K.fan && K.n_views <= 1 ? 1 : 0);
+    // ... and single frames of the opaque-scene kernel over 16 tiles (4 pixels of each per wave; round 4, with the
+    // direct group stack: C3 frame 1.06 ms vs 1.20 untouched, 1.14 over 64 tiles, profiles/r04/ab_r04n_interleave.log;
+    // over 64 tiles it had lost in round 3, 1.41 vs 1.33)
+    const bool opq_frame = K.n_views <= 1 && opaque_path(c, K, true);
+    const int il = c->opt_interleave >= 0 ? c->opt_interleave : (opq_frame ? 4 : (K.fan && K.n_views <= 1 ? 1 : 0));
+    K.interleave = il == 1 ? 6 : il;  // log2 of the tiles a wave's jobs spread over (option 1: 64 tiles)
     // single frames of the opaque-scene kernel start every XCD range at its rows nearest the image centre: the
     // frame's longest query chains (reflections inside the object) start first (C3 frame 1.40 -> 1.33 ms; the
     // 64-view batch and the fan renders, C4 / C5, gain nothing or lose: DESIGN.md section 6c)
