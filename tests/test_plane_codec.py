@@ -1,0 +1,37 @@
+"""The BVH8 child-plane words both builders write (bvh_build.h plane_q / plane_down / plane_up, RT_PLANES_F16):
+an IEEE binary16 value per word, a child's lo plane rounded down and its hi plane rounded up on that grid -- the
+conservative rounding the traversal's culling relies on.  Checked against numpy's float16
+on the host build of the header."""
+import os
+import subprocess
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_plane_words_are_conservative_halves(tmp_path):
+    exe = str(tmp_path / "plane_codec")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-I", os.path.join(REPO, "raytracer-group27_amd",
+                    "csrc"), os.path.join(REPO, "tests", "cpp", "plane_codec.cpp"), "-o", exe], check=True)
+    rng = np.random.default_rng(16)
+    xs = np.concatenate([[0.0, 1e-9, 6e-8, 1.0, 2047.5, 2048.0, 2049.0, 65000.0, 65504.0, 70000.0],
+                         rng.uniform(0, 65504, 4000), rng.uniform(0, 2, 2000), 2.0 ** rng.uniform(-24, 16, 2000)])
+    out = subprocess.run([exe], input="\n".join(repr(float(x)) for x in xs), capture_output=True, text=True,
+                         check=True).stdout.split("\n")
+    for x, line in zip(xs, out):
+        d, u, vd, vu = line.split()
+        d, u, vd, vu = int(d), int(u), float(vd), float(vu)
+        assert 0 <= d <= 0x7BFF and 0 <= u <= 0x7BFF, (x, d, u)
+        # the words are the binary16 bit patterns of their values
+        assert float(np.array([d], np.uint16).view(np.float16)[0]) == vd, (x, d)
+        assert float(np.array([u], np.uint16).view(np.float16)[0]) == vu, (x, u)
+        if x <= 65504.0:
+            assert vd <= x <= vu, (x, vd, vu)  # outward rounding
+            # tight: the neighbouring words are on the other side of x
+            if d < 0x7BFF:
+                assert float(np.array([d + 1], np.uint16).view(np.float16)[0]) > x, (x, d)
+            if u > 0:
+                assert float(np.array([u - 1], np.uint16).view(np.float16)[0]) < x, (x, u)
+        else:
+            assert d == u == 0x7BFF
