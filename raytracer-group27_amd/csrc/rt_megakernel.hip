@@ -1001,8 +1001,7 @@ __device__ __attribute__((noinline)) bool advance_lane_call(const void* ka, Lane
 
 #define RT_V_W3 8    // compiled for 3 waves per SIMD (168 VGPRs)
 #define RT_V_REVISIT 32  // opaque / tree kernels: the re-visit group stack of the other kernels (A/B), not DIRECT
-#define RT_V_W5 128  // compiled for 5 waves per SIMD (~102 VGPRs; A/B builds)
-#define RT_V_WAVES(V) (((V) & RT_V_W5) ? 5 : ((V) & RT_V_W4) ? 4 : ((V) & RT_V_W3) ? 3 : 2)
+#define RT_V_WAVES(V) (((V) & RT_V_W4) ? 4 : ((V) & RT_V_W3) ? 3 : 2)
 
 
 template <bool COUNT, bool TEX, int V>

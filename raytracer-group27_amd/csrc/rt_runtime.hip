@@ -104,7 +104,7 @@ struct rt_ctx {
     bool df_ok = true;  // the BVH8 fits the dynamic-fetch kernel's LDS stack
     bool glossy_material = false;  // opaque, ks > 0, shininess != 0 (glossy_ray_count > 1 draws lobes)
     int persistent_blocks[1024] = {0};  // resident 64-lane blocks per (kernel class, variant)
-    int opaque_blocks[3] = {0, 0, 0};   // ... of the opaque-scene kernel (4, 3, 5 waves per SIMD)
+    int opaque_blocks[2] = {0, 0};      // ... of the opaque-scene kernel (4 / 3 waves per SIMD)
     int tree_blocks[2] = {0, 0};        // ... of the recursion-tree kernel
     // recursion-tree kernel: the lanes' pending refracted rays (KParams::frames)
     float* d_frames = nullptr;
@@ -919,7 +919,7 @@ static int set_option_one(rt_ctx* c, int option, int value) {
             c->opt_variant = value;
             return RT_OK;
         case RT_OPT_OPAQUE:
-            if (value < -1 || value > 4) break;
+            if (value < -1 || value > 3) break;
             c->opt_opaque = value;
             return RT_OK;
         case RT_OPT_TREE:
@@ -986,7 +986,6 @@ static bool use_df(const rt_ctx* c, const KParams& K) {
 // 3 (their tail is a few waves' serial chains, which run faster with more registers: 1.40-1.45 vs 1.56-1.63 ms)
 #define RT_OPAQUE_V (RT_V_W4 | RT_V_NOPF)
 #define RT_OPAQUE_V3 (RT_V_W3 | RT_V_NOPF)
-#define RT_OPAQUE_V5 (RT_V_W5 | RT_V_NOPF)
 
 // Renders that the opaque-scene kernel draws: pixels (not rt_shade's explicit rays) of a large scene
 // (the dynamic-fetch class) whose materials are all opaque, lit by point and spot lights only, without
@@ -1004,7 +1003,6 @@ static int opaque_variant(const rt_ctx* c, const KParams& K) {
     (void)K;
     if (c->opt_opaque == 2) return RT_OPAQUE_V3;
     if (c->opt_opaque == 3) return RT_OPAQUE_V | RT_V_REVISIT;
-    if (c->opt_opaque == 4) return RT_OPAQUE_V5;
     return RT_OPAQUE_V;
 }
 
@@ -1061,8 +1059,6 @@ static int launch_persistent(int grid, hipStream_t st, const KParams& K, const J
         if (v == (RT_OPAQUE_V | RT_V_REVISIT)) {  // A/B: the 4-wave build with the re-visit group stack
             hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V | RT_V_REVISIT>), dim3(grid), dim3(64), 0, st,
                                K, J);
-        } else if (v == RT_OPAQUE_V5) {  // A/B: 5 waves per SIMD
-            hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V5>), dim3(grid), dim3(64), 0, st, K, J);
         } else if (v == RT_OPAQUE_V3) {
             hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V3>), dim3(grid), dim3(64), 0, st, K, J);
         } else {
@@ -1112,14 +1108,13 @@ static int occupancy_of(int* per_cu) {
 static int persistent_grid(rt_ctx* c, const KParams& K, bool pixels) {
     if (opaque_path(c, K, pixels)) {
         const int v = opaque_variant(c, K);
-        const int key = (v & RT_V_W3) ? 1 : (v & RT_V_W5) ? 2 : 0;  // 3, 5 or 4 waves per SIMD
+        const int key = (v & RT_V_W3) ? 1 : 0;  // 3 or 4 waves per SIMD
         if (c->opaque_blocks[key] > 0) return c->opaque_blocks[key];
         int cus = 0, per_cu = 0;
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
         const hipError_t e =
-            key == 1   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V3>, 64, 0)
-            : key == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V5>, 64, 0)
-                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V>, 64, 0);
+            key ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V3>, 64, 0)
+                : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V>, 64, 0);
         if (e != hipSuccess || per_cu <= 0) per_cu = 8;
         c->opaque_blocks[key] = std::max(1, cus) * per_cu;
         return c->opaque_blocks[key];
