@@ -103,6 +103,7 @@ struct KParams {
     int shade_level;            // rt_shade: recursion level of the explicit rays (getFinalColor's `level`)
     int fan;                    // dynamic-fetch kernel: bit 0 spherical-, bit 1 plane-light samples as wave-shared fans
     int interleave;             // job -> pixel: 0 a wave's 64 jobs are one 8x8 tile; k > 0 they spread over 2^k tiles
+    int interleave_view;        // ... in the views from this one on (a batch's last views: its drain)
     int centre_first;           // job -> tile: the upper half's per-XCD tile ranges walked bottom-up (single frames)
     int fan_cap;                // ... a wave with this many pixels waiting on fans takes no new pixels
     int dual;                   // dynamic-fetch kernel: a lane testing a leaf's records also visits its next node

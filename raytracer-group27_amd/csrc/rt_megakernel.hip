@@ -816,7 +816,7 @@ __device__ __forceinline__ void queue_camera(const KParams& P, Lane& L, Query& q
 __device__ __forceinline__ bool job_pixel(const KParams& P, int gjob, uint32_t& rpix, int& out_row) {
     int view;
     int job = view_job(P, gjob, view);
-    if (P.interleave) {
+    if (P.interleave && view >= P.interleave_view) {
         // groups of k = 2^interleave tiles: the group's r-th job is pixel r / nb of its tile r % nb, so the
         // 64 jobs one wave takes lie in k tiles (64 / k pixels of each), and an expensive patch of the image
         // is shared by k waves instead of held by one

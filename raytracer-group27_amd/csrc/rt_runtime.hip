@@ -129,6 +129,7 @@ struct rt_ctx {
     int opt_wave_trace = 0;
     int opt_fan = 1;        // dynamic-fetch kernel: spherical-light samples as wave-shared fans
     int opt_interleave = -1;  // job -> pixel interleave: -1 by render shape, 0 off, 1 over 64 tiles, 2..6 over 2^k
+    int opt_il_tail = 0;      // opaque batches: their last views interleaved over 16 tiles (RT_OPT_INTERLEAVE_TAIL)
     int opt_centre_first = -1;  // job -> tile: upper ranges bottom-up: -1 by render shape, 0 off, 1 on
     int opt_fan_cap = 0;      // pixels a wave may have waiting on fans before it stops taking new ones (0: default)
     int opt_dual = -1;        // dynamic-fetch steps: record and node visit in one iteration (-1 default, 0 off, 1 on)
@@ -930,6 +931,10 @@ static int set_option_one(rt_ctx* c, int option, int value) {
             if (value < -1 || value > 0) break;
             c->opt_peer = value;
             return RT_OK;
+        case RT_OPT_INTERLEAVE_TAIL:
+            if (value < 0 || value > 65535) break;
+            c->opt_il_tail = value;
+            return RT_OK;
         default:
             set_error("rt_ctx_set_option: unknown option");
             return RT_ERR_INVALID;
@@ -1293,9 +1298,16 @@ static void shape_options(const rt_ctx* c, KParams& K) {
     // ... and single frames of the opaque-scene kernel over 16 tiles (4 pixels of each per wave; round 4, with the
     // direct group stack: C3 frame 1.06 ms vs 1.20 untouched, 1.14 over 64 tiles, profiles/r04/ab_r04n_interleave.log;
     // over 64 tiles it had lost in round 3, 1.41 vs 1.33)
-    const bool opq_frame = K.n_views <= 1 && opaque_path(c, K, true);
+    const bool opq = opaque_path(c, K, true), opq_frame = K.n_views <= 1 && opq;
     const int il = c->opt_interleave >= 0 ? c->opt_interleave : (opq_frame ? 4 : (K.fan && K.n_views <= 1 ? 1 : 0));
     K.interleave = il == 1 ? 6 : il;  // log2 of the tiles a wave's jobs spread over (option 1: 64 tiles)
+    K.interleave_view = 0;
+    // opaque-kernel batches: the last RT_OPT_INTERLEAVE_TAIL views (the launch's drain) over 16 tiles, the rest
+    // in tile order (a whole batch interleaved loses its coherence: 64 views 0.625 vs 0.407 ms/frame)
+    if (opq && K.n_views > 1 && c->opt_interleave < 0 && c->opt_il_tail > 0) {
+        K.interleave = 4;
+        K.interleave_view = std::max(0, K.n_views - c->opt_il_tail);
+    }
     // single frames of the opaque-scene kernel start every XCD range at its rows nearest the image centre: the
     // frame's longest query chains (reflections inside the object) start first (C3 frame 1.40 -> 1.33 ms; the
     // 64-view batch and the fan renders, C4 / C5, gain nothing or lose: DESIGN.md section 6c)
