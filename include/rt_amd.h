@@ -366,7 +366,8 @@ int rt_update_materials(rt_ctx* ctx, int num_meshes, const rt_material* material
  * roofline accounting (process-wide switch). */
 int rt_set_counting(int on);
 /* Developer counters of the last counting launch (up to 32 words; [8..11] state-machine / traversal clocks,
- * [16..18] node re-visits of popped stack groups, their slots, their slots still hit). */
+ * [16..18] node re-visits of popped stack groups, their slots, their slots still hit; [24] / [25] the first
+ * out-of-range index of a checked build (code << 32 | value) and their count). */
 int rt_debug_counters(rt_ctx* ctx, uint64_t* out, int n);
 /* Context options: test and developer hooks (the library reads no environment variables).  The
  * defaults are the shipped path; every setting renders the same image and ray count. */
@@ -382,7 +383,7 @@ int rt_debug_counters(rt_ctx* ctx, uint64_t* out, int n);
 #define RT_OPT_DUAL_STEP 10  /* dynamic-fetch kernel: a lane testing leaf records also visits its next node in the same step (-1 default = 1, 0 off) */
 #define RT_OPT_CENTRE_FIRST 12 /* job order: the per-XCD tile ranges above the image centre walked bottom-up, so every range starts at its rows nearest the centre: -1 by render shape, 0 off, 1 on */
 #define RT_OPT_OPAQUE 11     /* opaque-scene kernel (opaque materials, point / spot lights, no lobes or textures): -1 where eligible (the 4-wave build), 0 never, 1 the 4-wave build, 2 the 3-wave build, 3 the 4-wave build with the re-visit group stack (A/Bs) */
-#define RT_OPT_TREE 13       /* recursion-tree kernel (transparent materials, all four light types with <= 64-sample fans, no lobes or textures): -1 / 2 where eligible, 0 never, 1 its build with the re-visit group stack (A/B) */
+#define RT_OPT_TREE 13       /* recursion-tree kernel (transparent materials, all four light types with <= 64-sample fans, no lobes or textures): -1 / 2 where eligible, 0 never, 1 its build with the re-visit group stack (A/B), 3 a checked 4-wave build (developer diagnosis: out-of-range indices reported in rt_debug_counters [24] / [25] instead of accessed) */
 #define RT_OPT_PEER_STORES 14 /* split renders: -1 the replicas with peer access to devices[0] store their pixels straight into its images (default), 0 every replica renders band-dense on its own device and copies (the path of devices without peer access) */
 #define RT_OPT_INTERLEAVE_TAIL 15 /* opaque-kernel view batches: the last n views' jobs spread over 16 tiles per wave (the launch's drain), the others in tile order; 0 none */
 #define RT_KERNEL_AUTO 0

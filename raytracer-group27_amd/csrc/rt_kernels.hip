@@ -63,6 +63,7 @@ struct DevScene {
     const DSpot* __restrict__ spot;
     const rt_plane_light* __restrict__ plane;
     int ntri, nsph, nref;
+    int nnodes;      // BVH8 nodes (the checked builds' bounds)
     int npl, nsl, nspot, nplane;
     int all_opaque;  // every mesh and sphere material has transparency == 1.0f
     // kd textures (Image, src/image.cpp): texels (r, g, b) of every level of every texture;

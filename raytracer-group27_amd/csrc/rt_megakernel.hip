@@ -1001,6 +1001,7 @@ __device__ __attribute__((noinline)) bool advance_lane_call(const void* ka, Lane
 
 #define RT_V_W3 8    // compiled for 3 waves per SIMD (168 VGPRs)
 #define RT_V_REVISIT 32  // opaque / tree kernels: the re-visit group stack of the other kernels (A/B), not DIRECT
+#define RT_V_CHK 64      // tree kernel: the checked build (indices validated and reported, chk_report)
 #define RT_V_WAVES(V) (((V) & RT_V_W4) ? 4 : ((V) & RT_V_W3) ? 3 : 2)
 
 
@@ -1171,14 +1172,31 @@ __device__ __forceinline__ void node_fetch(const float4* nodes, uint32_t cur, fl
 // at once into g), and the hit leaf slots postponed into T.lb/lc/lh.
 // PF: the node was prefetched into g by the previous visit (and the next one is prefetched here);
 // otherwise it is loaded now (fewer live registers).
+// Checked builds (RT_V_CHK, developer diagnosis of a fault): an index about to leave its buffer is reported
+// into err[0] (the first: code << 32 | value) and err[1] (a count) and the access is skipped, so the launch
+// finishes and says what it found instead of faulting.
+__device__ __forceinline__ void chk_report(unsigned long long* err, uint32_t code, uint32_t value) {
+    if (!err) return;
+    atomicCAS(err, 0ull, ((unsigned long long)code << 32) | value);
+    atomicAdd(err + 1, 1ull);
+}
+
 // DIRECT (the opaque and tree kernels): the stack holds groups of children, (child_base << 9) | (order << 8) |
 // slots (the builders put the inner children in the low slots, bvh_build.h slot_order, so a child's node is
 // child_base + slot), and a pop takes the group's next child at once -- front to back along the node's sort
 // axis by the ray's direction (order bit) -- where the re-visit form (node << 8) | slots re-tests the parent's
 // remaining slots first (one more node visit per pop).  Either walk gives the same lexicographic minimum.
-template <bool COUNT, int NW, bool PF = true, bool DIRECT = false>
-__device__ __forceinline__ void trav_node(const DevScene& S, Trav& T, int* stk, float4 (&g)[8], Cnt& cnt) {
+template <bool COUNT, int NW, bool PF = true, bool DIRECT = false, bool CHK = false>
+__device__ __forceinline__ void trav_node(const DevScene& S, Trav& T, int* stk, float4 (&g)[8], Cnt& cnt,
+                                          unsigned long long* err = nullptr) {
     const uint32_t node = T.cur >> 8;
+    if (CHK && node >= (uint32_t)S.nnodes) {
+        chk_report(err, 1, T.cur);
+        T.cur = RT_TRAV_NONE;
+        T.rk = 0;
+        T.lh = 0u;
+        return;
+    }
     if (!PF) node_fetch(S.nodes, T.cur, g);
     const float4 f0 = g[0], f1 = g[1], qlx = g[2], qly = g[3], qlz = g[4], qhx = g[5], qhy = g[6], qhz = g[7];
     if (COUNT) {
@@ -1257,6 +1275,11 @@ __device__ __forceinline__ void trav_node(const DevScene& S, Trav& T, int* stk, 
         const uint32_t rest = ih & ~(1u << sbest);
         if (DIRECT) {
             if (rest) {
+                if (CHK && T.sp >= RT_STACK8) {
+                    chk_report(err, 2, (uint32_t)T.sp);
+                    T.cur = RT_TRAV_NONE;
+                    return;
+                }
                 stk[T.sp * RT_WAVE] = (int)((child_base << 9) | (back << 8) | rest);
                 ++T.sp;
             }
@@ -1292,8 +1315,8 @@ __device__ __forceinline__ void trav_node(const DevScene& S, Trav& T, int* stk, 
 // One postponed leaf record (the loop body of test_records).  The cursor moves to the next hit
 // leaf slot when the current range is used up.  Any-hit queries drop the rest of their work on
 // the first accepted candidate.
-template <bool COUNT, bool PIN>
-__device__ __forceinline__ void trav_record(const DevScene& S, Trav& T, Cnt& cnt) {
+template <bool COUNT, bool PIN, bool CHK = false>
+__device__ __forceinline__ void trav_record(const DevScene& S, Trav& T, Cnt& cnt, unsigned long long* err = nullptr) {
     if (T.rk == 0) {
         const int s = __ffs(T.lh) - 1;
         T.lh &= T.lh - 1u;
@@ -1307,6 +1330,12 @@ __device__ __forceinline__ void trav_record(const DevScene& S, Trav& T, Cnt& cnt
     const int r = T.rr;
     T.rr = r + 1;
     T.rk--;
+    if (CHK && (r < 0 || r >= S.ntri)) {
+        chk_report(err, 3, (uint32_t)r);
+        T.rk = 0;
+        T.lh = 0u;
+        return;
+    }
     float4 r0, r1, r2, r3;
     load_record<PIN>(S.tri + r * 4, r0, r1, r2, r3);
     if (COUNT) {
@@ -2640,11 +2669,16 @@ enum { TA_DONE = 0, TA_QUERY = 1, TA_FAN = 2 };
 // else the path query (q = its ray, hit / b = its result) ended.  TA_QUERY with the next query in q
 // (sdist / sI: a cansee segment's distance and intensity), TA_FAN when a fan is to be posted, TA_DONE when
 // the job is complete.
-template <bool COUNT>
+template <bool COUNT, bool CHK = false>
 __device__ __forceinline__ int tree_advance(const KParams& P, TreeLane& L, int vis, const FanResult& fan, bool hit,
                                             const Best& b, Query& q, float& sdist, float& sI, Cnt& cnt) {
     const DevScene& S = P.S;
     bool node_done = true;
+    unsigned long long* err = CHK ? P.stats + RT_STATS_EXTRA + 8 : nullptr;
+    if (CHK && !fan.done && !L.shadow && hit && !(b.rec >= 0 ? b.rec < S.ntri : (-b.rec - 1) < S.nsph)) {
+        chk_report(err, 7, (uint32_t)b.rec);
+        hit = false;
+    }
     if (fan.done) {
         tree_fan_light(P, L, fan);
         L.li++;
@@ -2684,7 +2718,9 @@ __device__ __forceinline__ int tree_advance(const KParams& P, TreeLane& L, int v
                 const float refrC = 1.0f - reflC;
                 L.desc = true;
                 L.rc = reflC;
-                if (r * r * (1.0f - c * c) <= 1.0f) {
+                if (CHK && (int)L.nfr >= max(1, P.max_level)) {
+                    chk_report(err, 4, L.nfr);
+                } else if (r * r * (1.0f - c * c) <= 1.0f) {
                     const v3 fo = L.hp + 0.01f * refr, fw = L.w * refrC;
                     float4* fp = tree_frame(P, (int)L.nfr);
                     fp[0] = make_float4(fo.x, fo.y, fo.z, __int_as_float((int)L.level + 1));
@@ -2733,6 +2769,17 @@ __device__ __forceinline__ int tree_advance(const KParams& P, TreeLane& L, int v
         return TA_QUERY;
     }
     // camera sample complete
+    if (CHK) {
+        uint32_t rpix;
+        int out_row;
+        job_pixel(P, L.job, rpix, out_row);
+        const int rows = P.out_image ? max(1, P.n_views) * P.H : (P.view_rows > 0 ? max(1, P.n_views) * P.view_rows : 0x7FFFFFFF);
+        if (out_row < 0 || out_row >= rows || (int)(rpix % (uint32_t)P.W) >= P.W) {
+            chk_report(err, 5, (uint32_t)out_row);
+            L.job = -1;
+            return TA_DONE;
+        }
+    }
     if (store_sample(P, L.job, L.sample, L.acc)) {
         L.sample++;
         uint32_t rpix;
@@ -2751,7 +2798,7 @@ __device__ __forceinline__ int tree_advance(const KParams& P, TreeLane& L, int v
 
 template <bool COUNT, int V>
 __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_tree_kernel(KParams, JobSrc) {
-    constexpr bool PF = !(V & RT_V_NOPF), DIRECT = !(V & RT_V_REVISIT);
+    constexpr bool PF = !(V & RT_V_NOPF), DIRECT = !(V & RT_V_REVISIT), CHK = (V & RT_V_CHK) != 0;
     const void* ka = (const void*)__builtin_amdgcn_kernarg_segment_ptr();
 #define RT_FRESH const KParams& P = *(const KParams*)fresh_kernarg(ka); const DevScene& S = P.S
     __shared__ int stack_lds[RT_STACK8 * RT_WAVE];
@@ -2821,7 +2868,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_tree_kernel(KPar
                 q.d = T.d;
             }
             const int jb = L.job;
-            const int r = tree_advance<COUNT>(P, L, vis, fan, T.found, T.best, q, qsdist, qsI, cnt);
+            const int r = tree_advance<COUNT, CHK>(P, L, vis, fan, T.found, T.best, q, qsdist, qsI, cnt);
             if (r == TA_QUERY) {
                 start = true;
                 qshadow = L.shadow;
@@ -2895,6 +2942,10 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_tree_kernel(KPar
                     base += take;
                 }
                 __syncthreads();
+            }
+            if (CHK && tfree && ray_fan >= 0 && (ray_fan >= FAN_SLOTS || ray_s < 0 || ray_s >= 64)) {
+                chk_report(P.stats + RT_STATS_EXTRA + 8, 6, (uint32_t)(ray_fan << 8 | ray_s));
+                ray_fan = -1;
             }
             if (tfree && ray_fan >= 0) {
                 const v3 hp{ft.hx[ray_fan], ft.hy[ray_fan], ft.hz[ray_fan]};
@@ -2989,9 +3040,10 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_tree_kernel(KPar
             }
             if (tracing) {
                 const bool rec = leaf_pending(T);
-                if (rec) trav_record<COUNT, true>(S, T, cnt);
+                unsigned long long* err = CHK ? P.stats + RT_STATS_EXTRA + 8 : nullptr;
+                if (rec) trav_record<COUNT, true, CHK>(S, T, cnt, err);
                 const bool nv = T.cur != RT_TRAV_NONE && (!rec || (P.dual && T.lh == 0u));
-                if (nv) trav_node<COUNT, 8, PF, DIRECT>(S, T, stk, g, cnt);
+                if (nv) trav_node<COUNT, 8, PF, DIRECT, CHK>(S, T, stk, g, cnt, err);
             }
             if (tracing && !leaf_pending(T) && T.cur == RT_TRAV_NONE) {
                 trav_finish(S, T);

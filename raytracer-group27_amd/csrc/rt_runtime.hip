@@ -105,7 +105,7 @@ struct rt_ctx {
     bool glossy_material = false;  // opaque, ks > 0, shininess != 0 (glossy_ray_count > 1 draws lobes)
     int persistent_blocks[1024] = {0};  // resident 64-lane blocks per (kernel class, variant)
     int opaque_blocks[2] = {0, 0};      // ... of the opaque-scene kernel (4 / 3 waves per SIMD)
-    int tree_blocks[2] = {0, 0};        // ... of the recursion-tree kernel
+    int tree_blocks[3] = {0, 0, 0};     // ... of the recursion-tree kernel (3-wave, re-visit, checked 4-wave)
     // recursion-tree kernel: the lanes' pending refracted rays (KParams::frames)
     float* d_frames = nullptr;
     size_t frames_bytes = 0;
@@ -594,6 +594,7 @@ static int create_one(const rt_scene_desc* desc, int device, rt_ctx** out) {
     UP(mat_tex.data(), mat_tex.size(), S.mat_tex);
     S.ntex = desc->num_textures;
     S.ntri = ntri;
+    S.nnodes = c->nnodes;
     S.nsph = desc->num_spheres;
     S.nref = (int)refn.size();
     S.all_opaque = all_opaque ? 1 : 0;
@@ -924,7 +925,7 @@ static int set_option_one(rt_ctx* c, int option, int value) {
             c->opt_opaque = value;
             return RT_OK;
         case RT_OPT_TREE:
-            if (value < -1 || value > 2) break;
+            if (value < -1 || value > 3) break;
             c->opt_tree = value;
             return RT_OK;
         case RT_OPT_PEER_STORES:
@@ -1016,6 +1017,8 @@ static int opaque_variant(const rt_ctx* c, const KParams& K) {
 // C4 16-view batch at full size (round 4, gpurun_out/bench_r04b_C4.json) and is not compiled.
 #define RT_TREE_V3 (RT_V_W3 | RT_V_NOPF)
 #define RT_TREE_VR (RT_V_W3 | RT_V_NOPF | RT_V_REVISIT)  // A/B: the re-visit group stack (RT_OPT_TREE 1)
+// developer diagnosis of the 4-wave build's fault (RT_OPT_TREE 3): that build with every index checked (RT_V_CHK)
+#define RT_TREE_V4C (RT_V_W4 | RT_V_NOPF | RT_V_CHK)
 
 // Renders that the recursion-tree kernel draws: pixels of a dynamic-fetch-class render the opaque kernel
 // does not take, without textures or glossy lobes, whose spherical and plane lights fit one fan (<= 64
@@ -1028,7 +1031,9 @@ static bool tree_path(const rt_ctx* c, const KParams& K, bool pixels) {
     if (K.S.nplane > 0 && K.plane_k * K.plane_k > 64) return false;
     return (long long)K.S.npl + K.S.nsl + K.S.nspot + K.S.nplane < 65536;  // TreeLane::li
 }
-static int tree_variant(const rt_ctx* c) { return c->opt_tree == 1 ? RT_TREE_VR : RT_TREE_V3; }
+static int tree_variant(const rt_ctx* c) {
+    return c->opt_tree == 1 ? RT_TREE_VR : c->opt_tree == 3 ? RT_TREE_V4C : RT_TREE_V3;
+}
 
 // by render shape: view batches and sample-fan renders run the lean 4-wave variant (C4 single frame
 // with fans: 27.1 vs 30.3 ms), other single frames the 2-wave variant with the drain lane groups
@@ -1076,6 +1081,7 @@ static int launch_persistent(int grid, hipStream_t st, const KParams& K, const J
     if (tree_path(c, K, J.mode == 0)) {
         const int v = tree_variant(c);
         if (v == RT_TREE_VR) hipLaunchKernelGGL((persistent_tree_kernel<COUNT, RT_TREE_VR>), dim3(grid), dim3(64), 0, st, K, J);
+        else if (v == RT_TREE_V4C) hipLaunchKernelGGL((persistent_tree_kernel<COUNT, RT_TREE_V4C>), dim3(grid), dim3(64), 0, st, K, J);
         else hipLaunchKernelGGL((persistent_tree_kernel<COUNT, RT_TREE_V3>), dim3(grid), dim3(64), 0, st, K, J);
         std::snprintf(c->last_kernel, sizeof(c->last_kernel), "rt::persistent_tree_kernel<%s, %d>",
                       COUNT ? "true" : "false", v);
@@ -1125,13 +1131,14 @@ static int persistent_grid(rt_ctx* c, const KParams& K, bool pixels) {
         return c->opaque_blocks[key];
     }
     if (tree_path(c, K, pixels)) {
-        const int key = tree_variant(c) == RT_TREE_VR ? 1 : 0;
+        const int key = tree_variant(c) == RT_TREE_VR ? 1 : tree_variant(c) == RT_TREE_V4C ? 2 : 0;
         if (c->tree_blocks[key] > 0) return c->tree_blocks[key];
         int cus = 0, per_cu = 0;
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
         const hipError_t e =
-            key ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_tree_kernel<false, RT_TREE_VR>, 64, 0)
-                : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_tree_kernel<false, RT_TREE_V3>, 64, 0);
+            key == 1   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_tree_kernel<false, RT_TREE_VR>, 64, 0)
+            : key == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_tree_kernel<false, RT_TREE_V4C>, 64, 0)
+                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_tree_kernel<false, RT_TREE_V3>, 64, 0);
         if (e != hipSuccess || per_cu <= 0) per_cu = 8;
         c->tree_blocks[key] = std::max(1, cus) * per_cu;
         return c->tree_blocks[key];
