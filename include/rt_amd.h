@@ -366,7 +366,8 @@ int rt_update_materials(rt_ctx* ctx, int num_meshes, const rt_material* material
  * roofline accounting (process-wide switch). */
 int rt_set_counting(int on);
 /* Developer counters of the last counting launch (up to 32 words; [8..11] state-machine / traversal clocks,
- * [16..18] node re-visits of popped stack groups, their slots, their slots still hit; [24] / [25] the first
+ * [16..18] node re-visits of popped stack groups, their slots, their slots still hit; [19] / [20] the opaque
+ * kernel's reference-box tests of candidate culling per lane / per wave step; [24] / [25] the first
  * out-of-range index of a checked build (code << 32 | value) and their count). */
 int rt_debug_counters(rt_ctx* ctx, uint64_t* out, int n);
 /* Context options: test and developer hooks (the library reads no environment variables).  The
@@ -417,6 +418,10 @@ int rt_debug_records(rt_ctx* ctx, float* out, int first, int count);
  * or -1, per object (triangles in scene order, then spheres) its leaf id and depth-first visit key (a
  * leaf's stored object list = its objects by key).  Null outputs are skipped; returns nref. */
 int rt_debug_ref_bvh(rt_ctx* ctx, float* boxes, int* node_leaf, int* obj_leaf, int* obj_key);
+/* Self-check of the kernels' reference slab test (src/ray_tracing.cpp:213-264), no context needed: for n
+ * (box [lo, hi], ray [origin, normalised direction]) pairs, out[i] = the IEEE-quotient answer (bit 0) |
+ * the quotient-bound answer << 1 (0 miss, 1 hit, 2 left to the IEEE quotients); device 0. */
+int rt_debug_slab_check(const float* boxes, const float* rays, int n, int* out);
 
 /* Introspection for tests / roofline accounting. */
 int rt_ctx_info(rt_ctx* ctx, int* num_nodes, int* num_tri_records, int* ref_bvh_nodes,

@@ -156,6 +156,9 @@ struct Cnt {
     // node visits that re-test a node popped from the stack (slot mask < 0xFF), the popped groups' slot
     // counts and how many of those slots still hit (counting builds: the cost of the re-visit scheme)
     uint32_t rv, rvk, rvj;
+    // reference-box tests of candidate culling (ref_slab): lane evaluations, the wave's executions (the most
+    // any lane did per record step) and the last record step's count on this lane (counting builds)
+    uint32_t slab, wslab, slab_step;
 };
 
 // true on the lowest active lane of the wave (counting builds: one count per wave instruction stream)
@@ -166,12 +169,55 @@ __device__ __forceinline__ bool wave_leader() {
 // ------------------------------------------------------------------------------------------
 // Reference slab test (src/ray_tracing.cpp:213-264), dir = normalize(ray.direction).
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ bool ref_slab(const DRefNode& b, v3 o, v3 nd) {
-    if (b.lo[0] == FLT_MAX && b.lo[1] == FLT_MAX && b.lo[2] == FLT_MAX && b.hi[0] == -FLT_MAX &&
-        b.hi[1] == -FLT_MAX && b.hi[2] == -FLT_MAX)
-        return false;
-    if (o.x > b.lo[0] && o.y > b.lo[1] && o.z > b.lo[2] && o.x < b.hi[0] && o.y < b.hi[1] && o.z < b.hi[2])
-        return true;  // origin strictly inside: hit (t is restored by intersectNode)
+// RT_SLAB_FILTER (default 1): the six IEEE divisions are first bounded by reciprocal products, and the exact
+// quotients are formed only for a ray whose answer the bounds leave open (ref_slab_bounds).
+#ifndef RT_SLAB_FILTER
+#define RT_SLAB_FILTER 1
+#endif
+
+// a numerator / denominator pair whose product bound below holds: no zero, denormal, overflow or NaN case
+__device__ __forceinline__ bool slab_den_ok(float d) { return fabsf(d) >= 0x1p-40f && fabsf(d) <= 0x1p40f; }
+__device__ __forceinline__ bool slab_num_ok(float a) {
+    return fabsf(a) <= 0x1p40f && (a == 0.0f || fabsf(a) >= 0x1p-40f);
+}
+
+// The slab test's answer from bounds on its quotients: 0 miss, 1 hit, 2 open (the exact test decides).
+// With a and d in slab_*_ok's ranges every quotient is a normal float or an exact zero.  q' = a * rcp(d)
+// (v_rcp_f32: 1 ulp; the product: 1/2 ulp) lies within 2^-21 |q'| of the correctly rounded a / d, so
+// [q' - 2^-18 |q'|, q' + 2^-18 |q'|] holds the reference's quotient (zero numerators give exact zeros).
+// Per axis the reference's min / max of the two quotients is the pair's order by numerator and the sign
+// of d (a correctly rounded division is monotonic in its numerator; equal quotients are the same either
+// way).  tin > tout is decided when the bounds of max(tin_k) and min(tout_k) do not overlap, and tout < 0
+// by the signs of the tout numerators and denominators (no quotient underflows to zero in range).
+__device__ __forceinline__ int ref_slab_bounds(const DRefNode& b, v3 o, v3 nd) {
+    const float a[6] = {b.lo[0] - o.x, b.hi[0] - o.x, b.lo[1] - o.y, b.hi[1] - o.y, b.lo[2] - o.z, b.hi[2] - o.z};
+    const float d[3] = {nd.x, nd.y, nd.z};
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) ok = ok && slab_den_ok(d[k]) && slab_num_ok(a[2 * k]) && slab_num_ok(a[2 * k + 1]);
+    if (!ok) return 2;
+    float in_lo = -FLT_MAX, in_hi = -FLT_MAX, out_lo = FLT_MAX, out_hi = FLT_MAX;
+    bool out_neg = false;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float r = __builtin_amdgcn_rcpf(d[k]);
+        const bool lo_first = (a[2 * k] <= a[2 * k + 1]) == (d[k] > 0.0f);
+        const float qi = (lo_first ? a[2 * k] : a[2 * k + 1]) * r;
+        const float qo = (lo_first ? a[2 * k + 1] : a[2 * k]) * r;
+        const float ei = fabsf(qi) * 0x1p-18f, eo = fabsf(qo) * 0x1p-18f;
+        in_lo = fmaxf(in_lo, qi - ei);
+        in_hi = fmaxf(in_hi, qi + ei);
+        out_lo = fminf(out_lo, qo - eo);
+        out_hi = fminf(out_hi, qo + eo);
+        out_neg = out_neg || qo < 0.0f;
+    }
+    if (in_lo > out_hi) return 0;     // tin > tout
+    if (!(in_hi <= out_lo)) return 2;  // open
+    return out_neg ? 0 : 1;            // tin <= tout: a hit unless tout < 0
+}
+
+// the slab test's quotient part (src/ray_tracing.cpp:220-260) with the reference's IEEE divisions
+__device__ __forceinline__ bool ref_slab_div(const DRefNode& b, v3 o, v3 nd) {
     const float txmin = (b.lo[0] - o.x) / nd.x;
     const float txmax = (b.hi[0] - o.x) / nd.x;
     const float tymin = (b.lo[1] - o.y) / nd.y;
@@ -187,6 +233,19 @@ __device__ __forceinline__ bool ref_slab(const DRefNode& b, v3 o, v3 nd) {
     const float tin = gmax(gmax(tinx, tiny), tinz);
     const float tout = gmin(gmin(toutx, touty), toutz);
     return !(tin > tout || tout < 0.0f);
+}
+
+__device__ __forceinline__ bool ref_slab(const DRefNode& b, v3 o, v3 nd) {
+    if (b.lo[0] == FLT_MAX && b.lo[1] == FLT_MAX && b.lo[2] == FLT_MAX && b.hi[0] == -FLT_MAX &&
+        b.hi[1] == -FLT_MAX && b.hi[2] == -FLT_MAX)
+        return false;
+    if (o.x > b.lo[0] && o.y > b.lo[1] && o.z > b.lo[2] && o.x < b.hi[0] && o.y < b.hi[1] && o.z < b.hi[2])
+        return true;  // origin strictly inside: hit (t is restored by intersectNode)
+    if (RT_SLAB_FILTER) {
+        const int f = ref_slab_bounds(b, o, nd);
+        if (f != 2) return f != 0;
+    }
+    return ref_slab_div(b, o, nd);
 }
 
 struct RefMask {
@@ -580,8 +639,8 @@ __device__ void flush_counters(const KParams& P, const Cnt& c) {
             for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
             if ((threadIdx.x & 63) == 0) atomicAdd(P.stats + 13 + k, v);
         }
-        const uint32_t xs[3] = {c.rv, c.rvk, c.rvj};
-        for (int k = 0; k < 3; ++k) {
+        const uint32_t xs[5] = {c.rv, c.rvk, c.rvj, c.slab, c.wslab};
+        for (int k = 0; k < 5; ++k) {
             unsigned long long v = xs[k];
             for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
             if ((threadIdx.x & 63) == 0) atomicAdd(P.stats + RT_STATS_EXTRA + k, v);

@@ -1327,6 +1327,7 @@ __device__ __forceinline__ void trav_record(const DevScene& S, Trav& T, Cnt& cnt
         T.rk = (int)((T.lc >> (4 * s)) & 15u);
         if (T.rk == 0) return;
     }
+    if (COUNT) cnt.slab_step = 0;
     const int r = T.rr;
     T.rr = r + 1;
     T.rk--;
@@ -1346,7 +1347,15 @@ __device__ __forceinline__ void trav_record(const DevScene& S, Trav& T, Cnt& cnt
     if (!tri_test(r0, r1, r2, r3, T.o, T.d, T.nd, t)) return;
     const int key = T.ref ? __float_as_int(r3.z) : __float_as_int(r3.y);
     if (T.any ? !(t <= T.tcull) : !(t < T.best.t || (t == T.best.t && key < T.best.key))) return;
-    if (T.ref && !leaf_reachable(S, __float_as_int(r3.w), T.o, T.nd, T.mask)) return;
+    if (T.ref) {
+        const uint32_t k0 = COUNT ? __popc(T.mask.known) : 0u;
+        const bool reach = leaf_reachable(S, __float_as_int(r3.w), T.o, T.nd, T.mask);
+        if (COUNT) {
+            cnt.slab_step = __popc(T.mask.known) - k0;
+            cnt.slab += cnt.slab_step;
+        }
+        if (!reach) return;
+    }
     T.best.t = t;
     T.best.key = key;
     T.best.rec = r;
@@ -2427,6 +2436,12 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
             if (tracing) {
                 const bool rec = leaf_pending(T);
                 if (rec) trav_record<COUNT, true>(S, T, cnt);
+                if (COUNT) {  // the wave's ref_slab executions this step: the most any lane did
+                    const uint32_t ns = rec ? cnt.slab_step : 0u;
+                    uint32_t w = 0u;
+                    for (uint32_t k = 0; k < 8u; ++k) w += __ballot(ns > k) ? 1u : 0u;
+                    if (wave_leader()) cnt.wslab += w;
+                }
                 const bool nv = T.cur != RT_TRAV_NONE && (!rec || (P.dual && T.lh == 0u));
                 if (nv) trav_node<COUNT, 8, PF, DIRECT>(S, T, stk, g, cnt);
             }

@@ -1709,6 +1709,46 @@ extern "C" int rt_render_views(rt_ctx* c, const rt_camera* cams, int n_views, co
     return RT_OK;
 }
 
+// the slab test's quotient bounds against its IEEE quotients, per (box, ray) pair (rt_debug_slab_check)
+__global__ void slab_check_kernel(const float* boxes, const float* rays, int n, int* out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    DRefNode b;
+    for (int k = 0; k < 3; ++k) {
+        b.lo[k] = boxes[6 * i + k];
+        b.hi[k] = boxes[6 * i + 3 + k];
+    }
+    const v3 o{rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]}, nd{rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]};
+    out[i] = (ref_slab_div(b, o, nd) ? 1 : 0) | (ref_slab_bounds(b, o, nd) << 1);
+}
+
+extern "C" int rt_debug_slab_check(const float* boxes, const float* rays, int n, int* out) {
+    if (n < 0 || (n > 0 && (!boxes || !rays || !out))) {
+        set_error("rt_debug_slab_check: invalid argument");
+        return RT_ERR_INVALID;
+    }
+    if (n == 0) return RT_OK;
+    float* d_b = nullptr;
+    int* d_o = nullptr;
+    HIP_TRY(hipMalloc(&d_b, sizeof(float) * 12 * (size_t)n));
+    hipError_t e = hipMalloc(&d_o, sizeof(int) * (size_t)n);
+    if (e == hipSuccess) e = hipMemcpy(d_b, boxes, sizeof(float) * 6 * (size_t)n, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d_b + 6 * (size_t)n, rays, sizeof(float) * 6 * (size_t)n, hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(slab_check_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, d_b, d_b + 6 * (size_t)n, n, d_o);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(out, d_o, sizeof(int) * (size_t)n, hipMemcpyDeviceToHost);
+    hipFree(d_b);
+    if (d_o) hipFree(d_o);
+    if (e != hipSuccess) {
+        set_error(std::string("rt_debug_slab_check: ") + hipGetErrorString(e));
+        return RT_ERR_HIP;
+    }
+    return RT_OK;
+}
+
 extern "C" int rt_intersect(rt_ctx* c, const rt_ray* rays, int n, int use_bvh, rt_hit* hits) {
     if (!c || n < 0 || (n > 0 && (!rays || !hits))) {
         set_error("rt_intersect: invalid argument");

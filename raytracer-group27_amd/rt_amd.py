@@ -136,7 +136,7 @@ EXPORTS = [
     "rt_philox4x32_10", "rt_debug_wave_trace", "rt_debug_job_trace", "rt_debug_create_ms", "rt_set_build_mode", "rt_debug_build_info", "rt_debug_records", "rt_debug_ref_bvh", "rt_decode_png", "rt_ctx_set_option", "rt_texture_sample",
     "rt_update_lights", "rt_update_materials", "rt_unpermute_views_device", "rt_scene_mesh_count", "rt_scene_mesh_get",
     "rt_ctx_devices", "rt_ctx_peer_stores", "rt_render_views_image_device", "rt_ipc_alloc", "rt_ipc_open", "rt_ipc_close", "rt_device_free",
-    "rt_device_synchronize", "rt_memcpy_dtoh",
+    "rt_device_synchronize", "rt_memcpy_dtoh", "rt_debug_slab_check",
 ]
 IPC_HANDLE_BYTES = 64
 
@@ -302,6 +302,7 @@ def lib():
             "rt_debug_build_info": ([vp, P(C.c_int), C.c_int], C.c_int),
             "rt_debug_records": ([vp, P(C.c_float), C.c_int, C.c_int], C.c_int),
             "rt_debug_ref_bvh": ([vp, P(C.c_float), P(C.c_int), P(C.c_int), P(C.c_int)], C.c_int),
+            "rt_debug_slab_check": ([P(C.c_float), P(C.c_float), C.c_int, P(C.c_int)], C.c_int),
             "rt_ctx_set_option": ([vp, C.c_int, C.c_int], C.c_int),
             "rt_texture_sample": ([vp, C.c_int, C.c_int, P(C.c_float), P(rt_params), P(C.c_float)], C.c_int),
             "rt_update_lights": ([vp, P(rt_scene_desc)], C.c_int),
@@ -679,6 +680,18 @@ class Context:
 
 def set_counting(on):
     check(lib().rt_set_counting(int(on)))
+
+
+def slab_check(boxes, rays):
+    """rt_debug_slab_check: per (box [lo, hi], ray [origin, normalised direction]) pair the kernels' slab test
+    by IEEE quotients (bit 0) and by quotient bounds (>> 1: 0 miss, 1 hit, 2 left to the quotients)."""
+    b = np.ascontiguousarray(boxes, np.float32).reshape(-1, 6)
+    r = np.ascontiguousarray(rays, np.float32).reshape(-1, 6)
+    assert len(b) == len(r)
+    out = np.zeros(len(b), np.int32)
+    check(lib().rt_debug_slab_check(b.ctypes.data_as(C.POINTER(C.c_float)), r.ctypes.data_as(C.POINTER(C.c_float)),
+                                    len(b), out.ctypes.data_as(C.POINTER(C.c_int))), "rt_debug_slab_check")
+    return out
 
 
 class IpcBuffer:

@@ -48,6 +48,8 @@ for cfg in cfgs:
               f"iterations by tracing lanes 1-16/17-32/33-64: "
               f"{[round(int(c[k]) / max(1, sum(int(c[j]) for j in (13, 14, 15))), 3) for k in (13, 14, 15)]} "
               f"revisits/ray={int(c[16]) / rays:.3f} (share of visits {int(c[16]) / max(1, nodes):.3f}, "
-              f"popped slots/revisit {int(c[17]) / max(1, int(c[16])):.2f}, still hit {int(c[18]) / max(1, int(c[16])):.2f})",
+              f"popped slots/revisit {int(c[17]) / max(1, int(c[16])):.2f}, still hit {int(c[18]) / max(1, int(c[16])):.2f}) "
+              f"ref_slab/ray={int(c[19]) / rays:.3f} wave ref_slab/ray={int(c[20]) / rays:.4f} "
+              f"(opaque kernel)",
               flush=True)
     ctx.close()
