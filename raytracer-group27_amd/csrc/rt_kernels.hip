@@ -156,9 +156,12 @@ struct Cnt {
     // node visits that re-test a node popped from the stack (slot mask < 0xFF), the popped groups' slot
     // counts and how many of those slots still hit (counting builds: the cost of the re-visit scheme)
     uint32_t rv, rvk, rvj;
-    // reference-box tests of candidate culling (ref_slab): lane evaluations, the wave's executions (the most
-    // any lane did per record step) and the last record step's count on this lane (counting builds)
-    uint32_t slab, wslab, slab_step;
+};
+
+// reference-box tests of candidate culling (ref_slab): lane evaluations, the wave's executions (the most any lane
+// did per record step) and the last record step's count on this lane (the opaque kernel's counting build)
+struct SlabCnt {
+    uint32_t slab, wslab, step;
 };
 
 // true on the lowest active lane of the wave (counting builds: one count per wave instruction stream)
@@ -170,50 +173,45 @@ __device__ __forceinline__ bool wave_leader() {
 // Reference slab test (src/ray_tracing.cpp:213-264), dir = normalize(ray.direction).
 // ------------------------------------------------------------------------------------------
 // RT_SLAB_FILTER (default 1): the six IEEE divisions are first bounded by reciprocal products, and the exact
-// quotients are formed only for a ray whose answer the bounds leave open (ref_slab_bounds).
+// quotients are formed only for a ray whose answer the bounds leave open (ref_slab_bounds).  Compiled into the
+// opaque and tree kernels' record tests (template FILTER); the general kernels keep the plain test (their
+// register allocation, which the filter's code perturbs, stays that of round 4's measured builds).
 #ifndef RT_SLAB_FILTER
 #define RT_SLAB_FILTER 1
 #endif
 
-// a numerator / denominator pair whose product bound below holds: no zero, denormal, overflow or NaN case
-__device__ __forceinline__ bool slab_den_ok(float d) { return fabsf(d) >= 0x1p-40f && fabsf(d) <= 0x1p40f; }
-__device__ __forceinline__ bool slab_num_ok(float a) {
-    return fabsf(a) <= 0x1p40f && (a == 0.0f || fabsf(a) >= 0x1p-40f);
-}
-
 // The slab test's answer from bounds on its quotients: 0 miss, 1 hit, 2 open (the exact test decides).
-// With a and d in slab_*_ok's ranges every quotient is a normal float or an exact zero.  q' = a * rcp(d)
+// In range (every |d| in [2^-40, 2^40], every |a| zero or in [2^-40, 2^40]; checked on the magnitude bits, so
+// NaN and infinity fall outside) every quotient is a normal float or an exact zero.  q' = a * rcp(d)
 // (v_rcp_f32: 1 ulp; the product: 1/2 ulp) lies within 2^-21 |q'| of the correctly rounded a / d, so
 // [q' - 2^-18 |q'|, q' + 2^-18 |q'|] holds the reference's quotient (zero numerators give exact zeros).
-// Per axis the reference's min / max of the two quotients is the pair's order by numerator and the sign
-// of d (a correctly rounded division is monotonic in its numerator; equal quotients are the same either
-// way).  tin > tout is decided when the bounds of max(tin_k) and min(tout_k) do not overlap, and tout < 0
-// by the signs of the tout numerators and denominators (no quotient underflows to zero in range).
+// Per axis the reference's min / max of the two quotients is the min / max of the two products (both
+// roundings are monotonic, and the products share the reciprocal; equal products bound both quotients).
+// tin > tout is decided when the bounds of max(tin_k) and min(tout_k) do not overlap, and tout < 0 by the
+// signs of the tout products (no quotient underflows to zero in range).
 __device__ __forceinline__ int ref_slab_bounds(const DRefNode& b, v3 o, v3 nd) {
-    const float a[6] = {b.lo[0] - o.x, b.hi[0] - o.x, b.lo[1] - o.y, b.hi[1] - o.y, b.lo[2] - o.z, b.hi[2] - o.z};
-    const float d[3] = {nd.x, nd.y, nd.z};
-    bool ok = true;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) ok = ok && slab_den_ok(d[k]) && slab_num_ok(a[2 * k]) && slab_num_ok(a[2 * k + 1]);
-    if (!ok) return 2;
-    float in_lo = -FLT_MAX, in_hi = -FLT_MAX, out_lo = FLT_MAX, out_hi = FLT_MAX;
-    bool out_neg = false;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const float r = __builtin_amdgcn_rcpf(d[k]);
-        const bool lo_first = (a[2 * k] <= a[2 * k + 1]) == (d[k] > 0.0f);
-        const float qi = (lo_first ? a[2 * k] : a[2 * k + 1]) * r;
-        const float qo = (lo_first ? a[2 * k + 1] : a[2 * k]) * r;
-        const float ei = fabsf(qi) * 0x1p-18f, eo = fabsf(qo) * 0x1p-18f;
-        in_lo = fmaxf(in_lo, qi - ei);
-        in_hi = fmaxf(in_hi, qi + ei);
-        out_lo = fminf(out_lo, qo - eo);
-        out_hi = fminf(out_hi, qo + eo);
-        out_neg = out_neg || qo < 0.0f;
-    }
-    if (in_lo > out_hi) return 0;     // tin > tout
+    const float a0x = b.lo[0] - o.x, a1x = b.hi[0] - o.x, a0y = b.lo[1] - o.y, a1y = b.hi[1] - o.y,
+                a0z = b.lo[2] - o.z, a1z = b.hi[2] - o.z;
+    auto mag = [](float x) { return __float_as_uint(x) & 0x7FFFFFFFu; };
+    constexpr uint32_t LO = 0x2B800000u, HI = 0x53800000u;  // 2^-40, 2^40
+    const uint32_t dmax = max(max(mag(nd.x), mag(nd.y)), mag(nd.z)), dmin = min(min(mag(nd.x), mag(nd.y)), mag(nd.z));
+    const uint32_t amax = max(max(max(mag(a0x), mag(a1x)), max(mag(a0y), mag(a1y))), max(mag(a0z), mag(a1z)));
+    // smallest nonzero magnitude: a zero maps to 0xFFFFFFFF
+    const uint32_t anz = min(min(min(mag(a0x) - 1u, mag(a1x) - 1u), min(mag(a0y) - 1u, mag(a1y) - 1u)),
+                             min(mag(a0z) - 1u, mag(a1z) - 1u));
+    if (!(dmax <= HI && dmin >= LO && amax <= HI && anz >= LO - 1u)) return 2;
+    const float rx = __builtin_amdgcn_rcpf(nd.x), ry = __builtin_amdgcn_rcpf(nd.y), rz = __builtin_amdgcn_rcpf(nd.z);
+    const float p0x = a0x * rx, p1x = a1x * rx, p0y = a0y * ry, p1y = a1y * ry, p0z = a0z * rz, p1z = a1z * rz;
+    const float ix = fminf(p0x, p1x), iy = fminf(p0y, p1y), iz = fminf(p0z, p1z);
+    const float ox = fmaxf(p0x, p1x), oy = fmaxf(p0y, p1y), oz = fmaxf(p0z, p1z);
+    constexpr float E = 0x1p-18f;
+    const float eix = fabsf(ix) * E, eiy = fabsf(iy) * E, eiz = fabsf(iz) * E;
+    const float eox = fabsf(ox) * E, eoy = fabsf(oy) * E, eoz = fabsf(oz) * E;
+    const float in_lo = fmaxf(fmaxf(ix - eix, iy - eiy), iz - eiz), in_hi = fmaxf(fmaxf(ix + eix, iy + eiy), iz + eiz);
+    const float out_lo = fminf(fminf(ox - eox, oy - eoy), oz - eoz), out_hi = fminf(fminf(ox + eox, oy + eoy), oz + eoz);
+    if (in_lo > out_hi) return 0;      // tin > tout
     if (!(in_hi <= out_lo)) return 2;  // open
-    return out_neg ? 0 : 1;            // tin <= tout: a hit unless tout < 0
+    return fminf(fminf(ox, oy), oz) < 0.0f ? 0 : 1;  // tin <= tout: a hit unless tout < 0
 }
 
 // the slab test's quotient part (src/ray_tracing.cpp:220-260) with the reference's IEEE divisions
@@ -235,13 +233,14 @@ __device__ __forceinline__ bool ref_slab_div(const DRefNode& b, v3 o, v3 nd) {
     return !(tin > tout || tout < 0.0f);
 }
 
+template <bool FILTER = false>
 __device__ __forceinline__ bool ref_slab(const DRefNode& b, v3 o, v3 nd) {
     if (b.lo[0] == FLT_MAX && b.lo[1] == FLT_MAX && b.lo[2] == FLT_MAX && b.hi[0] == -FLT_MAX &&
         b.hi[1] == -FLT_MAX && b.hi[2] == -FLT_MAX)
         return false;
     if (o.x > b.lo[0] && o.y > b.lo[1] && o.z > b.lo[2] && o.x < b.hi[0] && o.y < b.hi[1] && o.z < b.hi[2])
         return true;  // origin strictly inside: hit (t is restored by intersectNode)
-    if (RT_SLAB_FILTER) {
+    if (FILTER && RT_SLAB_FILTER) {
         const int f = ref_slab_bounds(b, o, nd);
         if (f != 2) return f != 0;
     }
@@ -252,6 +251,7 @@ struct RefMask {
     uint32_t known, pass;
 };
 
+template <bool FILTER = false>
 __device__ __forceinline__ bool leaf_reachable_p(const int* leaf_path, const DRefNode* refn, int leaf, v3 o, v3 nd,
                                                  RefMask& m) {
     const int* p = leaf_path + leaf * 8;
@@ -261,15 +261,16 @@ __device__ __forceinline__ bool leaf_reachable_p(const int* leaf_path, const DRe
         const uint32_t bit = 1u << node;
         if (!(m.known & bit)) {
             m.known |= bit;
-            if (ref_slab(refn[node], o, nd)) m.pass |= bit;
+            if (ref_slab<FILTER>(refn[node], o, nd)) m.pass |= bit;
         }
         if (!(m.pass & bit)) return false;
     }
     return true;
 }
 
+template <bool FILTER = false>
 __device__ __forceinline__ bool leaf_reachable(const DevScene& S, int leaf, v3 o, v3 nd, RefMask& m) {
-    return leaf_reachable_p(S.leaf_path, S.refn, leaf, o, nd, m);
+    return leaf_reachable_p<FILTER>(S.leaf_path, S.refn, leaf, o, nd, m);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -639,12 +640,24 @@ __device__ void flush_counters(const KParams& P, const Cnt& c) {
             for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
             if ((threadIdx.x & 63) == 0) atomicAdd(P.stats + 13 + k, v);
         }
-        const uint32_t xs[5] = {c.rv, c.rvk, c.rvj, c.slab, c.wslab};
-        for (int k = 0; k < 5; ++k) {
+        const uint32_t xs[3] = {c.rv, c.rvk, c.rvj};
+        for (int k = 0; k < 3; ++k) {
             unsigned long long v = xs[k];
             for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
             if ((threadIdx.x & 63) == 0) atomicAdd(P.stats + RT_STATS_EXTRA + k, v);
         }
+    }
+}
+
+// the opaque kernel's ref_slab counters (rt_debug_counters [19] / [20])
+template <bool COUNT>
+__device__ void flush_slab_counters(const KParams& P, const SlabCnt& c) {
+    if (!COUNT) return;
+    const uint32_t xs[2] = {c.slab, c.wslab};
+    for (int k = 0; k < 2; ++k) {
+        unsigned long long v = xs[k];
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if ((threadIdx.x & 63) == 0) atomicAdd(P.stats + RT_STATS_EXTRA + 3 + k, v);
     }
 }
 

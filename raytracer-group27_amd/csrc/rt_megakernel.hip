@@ -1315,8 +1315,10 @@ __device__ __forceinline__ void trav_node(const DevScene& S, Trav& T, int* stk, 
 // One postponed leaf record (the loop body of test_records).  The cursor moves to the next hit
 // leaf slot when the current range is used up.  Any-hit queries drop the rest of their work on
 // the first accepted candidate.
-template <bool COUNT, bool PIN, bool CHK = false>
-__device__ __forceinline__ void trav_record(const DevScene& S, Trav& T, Cnt& cnt, unsigned long long* err = nullptr) {
+// SLAB: the reference slab tests of candidate culling decided from quotient bounds first (RT_SLAB_FILTER)
+template <bool COUNT, bool PIN, bool CHK = false, bool SLAB = false>
+__device__ __forceinline__ void trav_record(const DevScene& S, Trav& T, Cnt& cnt, unsigned long long* err = nullptr,
+                                            SlabCnt* sc = nullptr) {
     if (T.rk == 0) {
         const int s = __ffs(T.lh) - 1;
         T.lh &= T.lh - 1u;
@@ -1327,7 +1329,7 @@ __device__ __forceinline__ void trav_record(const DevScene& S, Trav& T, Cnt& cnt
         T.rk = (int)((T.lc >> (4 * s)) & 15u);
         if (T.rk == 0) return;
     }
-    if (COUNT) cnt.slab_step = 0;
+    if (COUNT && sc) sc->step = 0;
     const int r = T.rr;
     T.rr = r + 1;
     T.rk--;
@@ -1348,11 +1350,11 @@ __device__ __forceinline__ void trav_record(const DevScene& S, Trav& T, Cnt& cnt
     const int key = T.ref ? __float_as_int(r3.z) : __float_as_int(r3.y);
     if (T.any ? !(t <= T.tcull) : !(t < T.best.t || (t == T.best.t && key < T.best.key))) return;
     if (T.ref) {
-        const uint32_t k0 = COUNT ? __popc(T.mask.known) : 0u;
-        const bool reach = leaf_reachable(S, __float_as_int(r3.w), T.o, T.nd, T.mask);
-        if (COUNT) {
-            cnt.slab_step = __popc(T.mask.known) - k0;
-            cnt.slab += cnt.slab_step;
+        const uint32_t k0 = (COUNT && sc) ? __popc(T.mask.known) : 0u;
+        const bool reach = leaf_reachable<SLAB>(S, __float_as_int(r3.w), T.o, T.nd, T.mask);
+        if (COUNT && sc) {
+            sc->step = __popc(T.mask.known) - k0;
+            sc->slab += sc->step;
         }
         if (!reach) return;
     }
@@ -2331,6 +2333,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
     L.shadow = false;
     Trav T;
     Cnt cnt{};
+    SlabCnt slab{};
     int xr = (int)(blockIdx.x & 7), xtried = 0;
     bool tracing = false, pending = false;
     unsigned long long t_exh = 0ull;
@@ -2435,12 +2438,12 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
             }
             if (tracing) {
                 const bool rec = leaf_pending(T);
-                if (rec) trav_record<COUNT, true>(S, T, cnt);
+                if (rec) trav_record<COUNT, true, false, true>(S, T, cnt, nullptr, COUNT ? &slab : nullptr);
                 if (COUNT) {  // the wave's ref_slab executions this step: the most any lane did
-                    const uint32_t ns = rec ? cnt.slab_step : 0u;
+                    const uint32_t ns = rec ? slab.step : 0u;
                     uint32_t w = 0u;
                     for (uint32_t k = 0; k < 8u; ++k) w += __ballot(ns > k) ? 1u : 0u;
-                    if (wave_leader()) cnt.wslab += w;
+                    if (wave_leader()) slab.wslab += w;
                 }
                 const bool nv = T.cur != RT_TRAV_NONE && (!rec || (P.dual && T.lh == 0u));
                 if (nv) trav_node<COUNT, 8, PF, DIRECT>(S, T, stk, g, cnt);
@@ -2518,6 +2521,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
     }
     const KParams& P = kernel_params(ka);
     flush_counters<COUNT>(P, cnt);
+    flush_slab_counters<COUNT>(P, slab);
     if (COUNT && P.wave_trace && lane_id == 0) {  // traces: counting build only
         unsigned long long* w = P.wave_trace + 8 * blockIdx.x;
         w[0] = t_wave0;
@@ -3056,7 +3060,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_tree_kernel(KPar
             if (tracing) {
                 const bool rec = leaf_pending(T);
                 unsigned long long* err = CHK ? P.stats + RT_STATS_EXTRA + 8 : nullptr;
-                if (rec) trav_record<COUNT, true, CHK>(S, T, cnt, err);
+                if (rec) trav_record<COUNT, true, CHK, true>(S, T, cnt, err);
                 const bool nv = T.cur != RT_TRAV_NONE && (!rec || (P.dual && T.lh == 0u));
                 if (nv) trav_node<COUNT, 8, PF, DIRECT, CHK>(S, T, stk, g, cnt, err);
             }

@@ -16,7 +16,8 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
-LIB_PATH = os.path.join(HERE, "librt_amd.so")
+_DEFAULT_LIB = os.path.join(HERE, "librt_amd.so")
+LIB_PATH = _DEFAULT_LIB
 # tools/sanitize/run.sh only: the CPU-only ASan/UBSan build of the host sources (its GPU entries are stubs
 # that fail with RT_ERR_NO_DEVICE, so nothing can pass on it that needs the GPU path)
 if os.environ.get("RT_AMD_SANITIZER_LIB"):
@@ -309,7 +310,11 @@ def lib():
             "rt_update_materials": ([vp, C.c_int, P(rt_material), C.c_int, P(rt_material)], C.c_int),
         }
         for name, (args, res) in sigs.items():
-            f = getattr(L, name)
+            f = getattr(L, name, None)
+            if f is None and LIB_PATH != _DEFAULT_LIB:  # an older A/B build (tools/ab_variants.py --lib)
+                continue
+            if f is None:
+                raise RtError(f"{LIB_PATH} does not export {name} (stale build: run raytracer-group27_amd/build.py)")
             f.argtypes = args
             f.restype = res
         _lib = L

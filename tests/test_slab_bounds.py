@@ -34,24 +34,22 @@ def ieee_answer(b, r):
 def bound_answer(b, r, rcp_ulps):
     """ref_slab_bounds with the reciprocal moved rcp_ulps (-1, 0, 1) ulps from 1/d: 0 miss, 1 hit, 2 open."""
     o, nd = r[:, :3], r[:, 3:]
-    a_lo, a_hi = b[:, :3] - o, b[:, 3:] - o
-    den_ok = (np.abs(nd) >= F(2.0 ** -40)) & (np.abs(nd) <= F(2.0 ** 40))
-
-    def num_ok(a):
-        return (np.abs(a) <= F(2.0 ** 40)) & ((a == 0) | (np.abs(a) >= F(2.0 ** -40)))
-
-    ok = np.all(den_ok & num_ok(a_lo) & num_ok(a_hi), axis=1)
+    a = np.concatenate([b[:, :3] - o, b[:, 3:] - o], 1)  # lo x y z, hi x y z
+    mag_d = nd.view(np.uint32) & np.uint32(0x7FFFFFFF)
+    mag_a = a.view(np.uint32) & np.uint32(0x7FFFFFFF)
+    LO, HI = np.uint32(0x2B800000), np.uint32(0x53800000)
+    ok = ((mag_d.max(1) <= HI) & (mag_d.min(1) >= LO) & (mag_a.max(1) <= HI) &
+          ((mag_a - np.uint32(1)).min(1) >= LO - np.uint32(1)))
     with np.errstate(divide="ignore", over="ignore", invalid="ignore"):
         rc = F(1.0) / nd
         if rcp_ulps:
             rc = np.nextafter(rc, np.where(rcp_ulps > 0, F(np.inf), F(-np.inf)).astype(F)).astype(F)
-        lo_first = (a_lo <= a_hi) == (nd > 0)
-        qi = np.where(lo_first, a_lo, a_hi) * rc
-        qo = np.where(lo_first, a_hi, a_lo) * rc
+        p0, p1 = a[:, :3] * rc, a[:, 3:] * rc
+        qi, qo = np.minimum(p0, p1), np.maximum(p0, p1)
         ei, eo = np.abs(qi) * F(2.0 ** -18), np.abs(qo) * F(2.0 ** -18)
         in_lo, in_hi = (qi - ei).max(axis=1), (qi + ei).max(axis=1)
         out_lo, out_hi = (qo - eo).min(axis=1), (qo + eo).min(axis=1)
-        out_neg = np.any(qo < 0, axis=1)
+        out_neg = qo.min(axis=1) < 0
     ans = np.where(in_lo > out_hi, 0, np.where(~(in_hi <= out_lo), 2, np.where(out_neg, 0, 1)))
     return np.where(ok, ans, 2)
 
