@@ -172,12 +172,14 @@ __device__ __forceinline__ bool wave_leader() {
 // ------------------------------------------------------------------------------------------
 // Reference slab test (src/ray_tracing.cpp:213-264), dir = normalize(ray.direction).
 // ------------------------------------------------------------------------------------------
-// RT_SLAB_FILTER (default 1): the six IEEE divisions are first bounded by reciprocal products, and the exact
-// quotients are formed only for a ray whose answer the bounds leave open (ref_slab_bounds).  Compiled into the
-// opaque and tree kernels' record tests (template FILTER); the general kernels keep the plain test (their
-// register allocation, which the filter's code perturbs, stays that of round 4's measured builds).
+// RT_SLAB_FILTER (A/B build option, default 0): the six IEEE divisions are first bounded by reciprocal products,
+// and the exact quotients are formed only for a ray whose answer the bounds leave open (ref_slab_bounds), in the
+// opaque and tree kernels' record tests (template FILTER).  Measured neutral (C3 16-view batch 0.445 / 0.443 vs
+// 0.447 / 0.444 ms/frame, C5 frame 152.4 vs 152.7 ms, profiles/r04/ab_r04s_slab.log: the culling's box tests are
+// 0.10 wave executions per ray, and the filter's code adds 10 spilled VGPRs to the 4-wave opaque build), so the
+// shipped kernels keep the plain test; rt_debug_slab_check checks the bounds either way.
 #ifndef RT_SLAB_FILTER
-#define RT_SLAB_FILTER 1
+#define RT_SLAB_FILTER 0
 #endif
 
 // The slab test's answer from bounds on its quotients: 0 miss, 1 hit, 2 open (the exact test decides).
