@@ -367,7 +367,8 @@ int rt_update_materials(rt_ctx* ctx, int num_meshes, const rt_material* material
 int rt_set_counting(int on);
 /* Developer counters of the last counting launch (up to 32 words; [8..11] state-machine / traversal clocks,
  * [16..18] node re-visits of popped stack groups, their slots, their slots still hit; [19] / [20] the opaque
- * kernel's reference-box tests of candidate culling per lane / per wave step; [24] / [25] the first
+ * kernel's reference-box tests of candidate culling per lane / per wave step, [21..23] its lane iterations held to a
+ * record test with a node to visit, with both a node visit and a record test, and in all; [24] / [25] the first
  * out-of-range index of a checked build (code << 32 | value) and their count). */
 int rt_debug_counters(rt_ctx* ctx, uint64_t* out, int n);
 /* Context options: test and developer hooks (the library reads no environment variables).  The

@@ -160,8 +160,11 @@ struct Cnt {
 
 // reference-box tests of candidate culling (ref_slab): lane evaluations, the wave's executions (the most any lane
 // did per record step) and the last record step's count on this lane (the opaque kernel's counting build)
+// ... and the traversal loop's lane iterations: tracing lanes, lanes with a node visit and a record test, lanes held
+// to a record test with a node to visit (their last visit's leaf hits still pending)
 struct SlabCnt {
     uint32_t slab, wslab, step;
+    uint32_t iters, both, blocked;
 };
 
 // true on the lowest active lane of the wave (counting builds: one count per wave instruction stream)
@@ -651,12 +654,12 @@ __device__ void flush_counters(const KParams& P, const Cnt& c) {
     }
 }
 
-// the opaque kernel's ref_slab counters (rt_debug_counters [19] / [20])
+// the opaque kernel's ref_slab and lane-iteration counters (rt_debug_counters [19..23])
 template <bool COUNT>
 __device__ void flush_slab_counters(const KParams& P, const SlabCnt& c) {
     if (!COUNT) return;
-    const uint32_t xs[2] = {c.slab, c.wslab};
-    for (int k = 0; k < 2; ++k) {
+    const uint32_t xs[5] = {c.slab, c.wslab, c.blocked, c.both, c.iters};
+    for (int k = 0; k < 5; ++k) {
         unsigned long long v = xs[k];
         for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
         if ((threadIdx.x & 63) == 0) atomicAdd(P.stats + RT_STATS_EXTRA + 3 + k, v);

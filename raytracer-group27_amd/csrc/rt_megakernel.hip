@@ -2446,6 +2446,11 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
                     if (wave_leader()) slab.wslab += w;
                 }
                 const bool nv = T.cur != RT_TRAV_NONE && (!rec || (P.dual && T.lh == 0u));
+                if (COUNT) {
+                    slab.iters++;
+                    if (nv && rec) slab.both++;
+                    if (!nv && T.cur != RT_TRAV_NONE) slab.blocked++;
+                }
                 if (nv) trav_node<COUNT, 8, PF, DIRECT>(S, T, stk, g, cnt);
             }
             if (tracing && !leaf_pending(T) && T.cur == RT_TRAV_NONE) {

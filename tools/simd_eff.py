@@ -50,6 +50,7 @@ for cfg in cfgs:
               f"revisits/ray={int(c[16]) / rays:.3f} (share of visits {int(c[16]) / max(1, nodes):.3f}, "
               f"popped slots/revisit {int(c[17]) / max(1, int(c[16])):.2f}, still hit {int(c[18]) / max(1, int(c[16])):.2f}) "
               f"ref_slab/ray={int(c[19]) / rays:.3f} wave ref_slab/ray={int(c[20]) / rays:.4f} "
-              f"(opaque kernel)",
+              f"lane iterations/ray={int(c[23]) / rays:.2f} (node + record {int(c[22]) / max(1, int(c[23])):.3f}, "
+              f"held to a record with a node to visit {int(c[21]) / max(1, int(c[23])):.3f}) (opaque kernel)",
               flush=True)
     ctx.close()
