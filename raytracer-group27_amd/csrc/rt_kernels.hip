@@ -122,7 +122,15 @@ struct KParams {
     // at frames + (f * frame_slots + s) * 3 (3 float4: origin + child level, direction, weight)
     float4* frames;
     int frame_slots;
+    // plane lights (fan renders): per light RT_PLANE_TAB float4 -- getPlaneLights' grid points px for k = 2..8
+    // (plane_tab_at), then normalize(cross(width, height)); built on the host with the loop's own additions
+    const float4* plane_tab;
 };
+
+// the plane-light table: grid points of every k in 2..8 (sum of k^2 = 203), then the light's normal
+#define RT_PLANE_TAB 204
+#define RT_PLANE_TAB_KMAX 8
+__host__ __device__ __forceinline__ int plane_tab_at(int k, int s) { return (k - 1) * k * (2 * k - 1) / 6 - 1 + s; }
 
 // Philox-4x32-10 (Salmon et al., SC'11; the Random123 constants): the counter-based stream that
 // replaces the reference's rand() for glossy lobes.  Counter = (draw, pixel, sample, 0).

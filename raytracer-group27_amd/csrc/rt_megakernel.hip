@@ -1736,7 +1736,7 @@ struct FanTable {
     float hx[FAN_SLOTS], hy[FAN_SLOTS], hz[FAN_SLOTS];  // the shading point
     int plane[FAN_SLOTS];                               // 1: a plane light's k * k grid, 0: a spherical light
     unsigned long long vis[FAN_SLOTS];                  // bit s: sample s visible
-    float rx[FAN_SLOTS], ry[FAN_SLOTS], rz[FAN_SLOTS];  // plane lights: the owner's reflected direction
+    float rx[FAN_SLOTS], ry[FAN_SLOTS], rz[FAN_SLOTS];  // plane lights: the owner's normalize(reflected direction)
     unsigned int c2max[FAN_SLOTS];                      // ... the visible samples' largest specular cosine (bits)
     float inten[FAN_SLOTS][64];                         // sample s's cansee intensity (transparent scenes)
     float term[FAN_SLOTS][64];                          // plane lights: visible sample s's hit term
@@ -1751,14 +1751,8 @@ __device__ __forceinline__ bool fan_sample_query(const KParams& P, v3 hp, int li
     if (plane) {
         // getPlaneLights' grid (src/shadow.cpp:259-299): row i = s / k, column j = s % k, px reached by
         // the loop's additions (py += dy per row, px += dx per column)
-        const rt_plane_light pl = P.S.plane[li];
-        const int k = P.plane_k, i = s / k, j = s % k;
-        const v3 w = ld3(pl.width), h = ld3(pl.height);
-        const v3 dx = (1.0f / (float)(k - 1)) * w, dy = (1.0f / (float)(k - 1)) * h;
-        v3 py = ld3(pl.position);
-        for (int r = 0; r < i; ++r) py = py + dy;
-        target = py;
-        for (int c = 0; c < j; ++c) target = target + dx;
+        const float4 t = P.plane_tab[li * RT_PLANE_TAB + plane_tab_at(P.plane_k, s)];
+        target = v3{t.x, t.y, t.z};
     } else {
     const rt_spherical_light sl = P.S.sl[li];
     const v3 lp = ld3(sl.position);
@@ -1789,18 +1783,16 @@ __device__ __forceinline__ bool fan_sample_query(const KParams& P, v3 hp, int li
 // instead of 64 serial normalisations on one lane.  maxCos = max(0, visible samples' cosines), NaN never
 // taken: an atomic maximum of the positive cosines' bits (positive floats order as their bits).
 __device__ __forceinline__ void fan_plane_term(const KParams& P, FanTable& ft, int f, int s) {
-    const rt_plane_light pl = P.S.plane[ft.li[f]];
-    const int k = P.plane_k, i = s / k, j = s % k;
-    const v3 w = ld3(pl.width), h = ld3(pl.height);
-    const v3 dx = (1.0f / (float)(k - 1)) * w, dy = (1.0f / (float)(k - 1)) * h;
-    v3 px = ld3(pl.position);
-    for (int r = 0; r < i; ++r) px = px + dy;
-    for (int c = 0; c < j; ++c) px = px + dx;
+    const float4* tab = P.plane_tab + ft.li[f] * RT_PLANE_TAB;
+    const float4 t = tab[plane_tab_at(P.plane_k, s)], nt = tab[RT_PLANE_TAB - 1];
+    const v3 px{t.x, t.y, t.z};
     const v3 hp{ft.hx[f], ft.hy[f], ft.hz[f]};
-    const v3 normal = normalize(cross(w, h));
+    const v3 normal{nt.x, nt.y, nt.z};
     const float dn = dot(normalize(hp - px), normal);
     ft.term[f][s] = ((dn < 0.0f) ? 0.0f : dn) / length(hp - px);
-    const float c2 = dot(normalize(v3{ft.rx[f], ft.ry[f], ft.rz[f]}), normalize(px - hp));
+    // normalize(px - hp) is -normalize(hp - px) bit for bit (a - b == -(b - a), and the products and sums of
+    // the dot product and the scaling negate exactly), so its cosine is the negated dot with that vector
+    const float c2 = -dot(v3{ft.rx[f], ft.ry[f], ft.rz[f]}, normalize(hp - px));
     if (c2 > 0.0f) atomicMax(&ft.c2max[f], __float_as_uint(c2));
 }
 
@@ -1951,9 +1943,10 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
                         ft.hx[f] = L.hp.x;
                         ft.hy[f] = L.hp.y;
                         ft.hz[f] = L.hp.z;
-                        ft.rx[f] = L.refl.x;
-                        ft.ry[f] = L.refl.y;
-                        ft.rz[f] = L.refl.z;
+                        const v3 nr = normalize(L.refl);  // (fan_plane_term's normalize(reflect), once per fan)
+                        ft.rx[f] = nr.x;
+                        ft.ry[f] = nr.y;
+                        ft.rz[f] = nr.z;
                         ft.c2max[f] = 0u;
                         own_fan = f;
                         fan_req = false;
@@ -2934,9 +2927,10 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_tree_kernel(KPar
                         ft.hx[f] = L.hp.x;
                         ft.hy[f] = L.hp.y;
                         ft.hz[f] = L.hp.z;
-                        ft.rx[f] = L.refl.x;
-                        ft.ry[f] = L.refl.y;
-                        ft.rz[f] = L.refl.z;
+                        const v3 nr = normalize(L.refl);  // (fan_plane_term's normalize(reflect), once per fan)
+                        ft.rx[f] = nr.x;
+                        ft.ry[f] = nr.y;
+                        ft.rz[f] = nr.z;
                         ft.c2max[f] = 0u;
                         own_fan = f;
                         fan_req = false;

@@ -108,6 +108,7 @@ struct rt_ctx {
     int tree_blocks[3] = {0, 0, 0};     // ... of the recursion-tree kernel (3-wave, re-visit, checked 4-wave)
     // recursion-tree kernel: the lanes' pending refracted rays (KParams::frames)
     float* d_frames = nullptr;
+    float4* d_plane_tab = nullptr;  // plane lights: their sample grids and normals (KParams::plane_tab)
     size_t frames_bytes = 0;
     // lights (re-uploadable: rt_update_lights)
     void* d_lights[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -280,6 +281,7 @@ extern "C" int rt_destroy(rt_ctx* c) {
     if (c->d_wave_trace) hipFree(c->d_wave_trace);
     if (c->d_views) hipFree(c->d_views);
     if (c->d_frames) hipFree(c->d_frames);
+    if (c->d_plane_tab) hipFree(c->d_plane_tab);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
     return RT_OK;
@@ -372,6 +374,35 @@ static int upload_lights(rt_ctx* c, const rt_scene_desc* d) {
     S.nsl = d->num_spherical_lights;
     S.nspot = d->num_spot_lights;
     S.nplane = d->num_plane_lights;
+    // getPlaneLights' sample points (src/shadow.cpp:259-299) for every grid size a fan takes (k = 2..8): px of row i,
+    // column j reached by the loop's own additions (py += dy per row, px += dx per column, dx = (1 / (k - 1)) * w),
+    // and the light's normalize(cross(w, h)) -- float arithmetic the kernels would repeat per sample
+    if (c->d_plane_tab) hipFree(c->d_plane_tab);
+    c->d_plane_tab = nullptr;
+    if (d->num_plane_lights > 0) {
+        std::vector<float4> tab((size_t)d->num_plane_lights * RT_PLANE_TAB);
+        for (int l = 0; l < d->num_plane_lights; ++l) {
+            const rt_plane_light& pl = d->plane_lights[l];
+            const v3 w{pl.width[0], pl.width[1], pl.width[2]}, h{pl.height[0], pl.height[1], pl.height[2]};
+            float4* t = tab.data() + (size_t)l * RT_PLANE_TAB;
+            for (int k = 2; k <= RT_PLANE_TAB_KMAX; ++k) {
+                const v3 dx = (1.0f / (float)(k - 1)) * w, dy = (1.0f / (float)(k - 1)) * h;
+                v3 py{pl.position[0], pl.position[1], pl.position[2]};
+                for (int i = 0; i < k; ++i) {
+                    v3 px = py;
+                    for (int j = 0; j < k; ++j) {
+                        t[plane_tab_at(k, i * k + j)] = make_float4(px.x, px.y, px.z, 0.0f);
+                        px = px + dx;
+                    }
+                    py = py + dy;
+                }
+            }
+            const v3 n = normalize(cross(w, h));
+            t[RT_PLANE_TAB - 1] = make_float4(n.x, n.y, n.z, 0.0f);
+        }
+        HIP_TRY(hipMalloc(&c->d_plane_tab, tab.size() * sizeof(float4)));
+        HIP_TRY(hipMemcpy(c->d_plane_tab, tab.data(), tab.size() * sizeof(float4), hipMemcpyHostToDevice));
+    }
     return RT_OK;
 }
 
@@ -1224,6 +1255,7 @@ static int fill_params(rt_ctx* c, const rt_camera* cam, const rt_params* p, int 
     K.seed_lo = (uint32_t)(p->rng_seed & 0xFFFFFFFFull);
     K.seed_hi = (uint32_t)(p->rng_seed >> 32);
     K.plane_k = p->plane_light_1D_ray_count;
+    K.plane_tab = c->d_plane_tab;
     K.use_bvh = p->use_bvh ? 1 : 0;
     K.refr = p->refraction_factor;
     // getSpherelights ring/spoke counts (src/shadow.cpp:190-195), host float math as the reference
