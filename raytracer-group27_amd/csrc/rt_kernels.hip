@@ -281,6 +281,46 @@ __device__ __forceinline__ bool leaf_reachable_p(const int* leaf_path, const DRe
     return true;
 }
 
+// The reference BVH in LDS (opaque and tree kernels, RT_REF_LDS): its <= 31 node boxes and every leaf's root path
+// packed in one word (count in bits 0-2, node ids in 5-bit fields; all ones: a path of more than 5 nodes, read from
+// device memory) -- the culling's loads without a device-memory round trip per path level
+struct RefLds {
+    DRefNode box[32];
+    uint32_t path[32];
+};
+__device__ __forceinline__ void ref_lds_load(const DevScene& S, RefLds& r, int lane) {
+    const float* src = reinterpret_cast<const float*>(S.refn);
+    float* dst = &r.box[0].lo[0];
+    for (int i = lane; i < S.nref * 6; i += 64) dst[i] = src[i];
+    if (lane < 32) {
+        const int* p = S.leaf_path + lane * 8;
+        const int cnt = p[0];
+        uint32_t w = 0xFFFFFFFFu;
+        if (cnt <= 5) {
+            w = (uint32_t)cnt;
+            for (int k = 0; k < cnt; ++k) w |= (uint32_t)p[1 + k] << (3 + 5 * k);
+        }
+        r.path[lane] = w;
+    }
+}
+template <bool FILTER = false>
+__device__ __forceinline__ bool leaf_reachable_lds(const DevScene& S, const RefLds& r, int leaf, v3 o, v3 nd,
+                                                   RefMask& m) {
+    const uint32_t w = r.path[leaf];
+    if (w == 0xFFFFFFFFu) return leaf_reachable_p<FILTER>(S.leaf_path, S.refn, leaf, o, nd, m);
+    const int cnt = (int)(w & 7u);
+    for (int k = 0; k < cnt; ++k) {
+        const int node = (int)((w >> (3 + 5 * k)) & 31u);
+        const uint32_t bit = 1u << node;
+        if (!(m.known & bit)) {
+            m.known |= bit;
+            if (ref_slab<FILTER>(r.box[node], o, nd)) m.pass |= bit;
+        }
+        if (!(m.pass & bit)) return false;
+    }
+    return true;
+}
+
 template <bool FILTER = false>
 __device__ __forceinline__ bool leaf_reachable(const DevScene& S, int leaf, v3 o, v3 nd, RefMask& m) {
     return leaf_reachable_p<FILTER>(S.leaf_path, S.refn, leaf, o, nd, m);

@@ -1315,10 +1315,14 @@ __device__ __forceinline__ void trav_node(const DevScene& S, Trav& T, int* stk, 
 // One postponed leaf record (the loop body of test_records).  The cursor moves to the next hit
 // leaf slot when the current range is used up.  Any-hit queries drop the rest of their work on
 // the first accepted candidate.
-// SLAB: the reference slab tests of candidate culling decided from quotient bounds first (RT_SLAB_FILTER)
+// SLAB: the reference slab tests of candidate culling decided from quotient bounds first (RT_SLAB_FILTER); rl: the
+// reference BVH in LDS (RT_REF_LDS)
+#ifndef RT_REF_LDS
+#define RT_REF_LDS 1
+#endif
 template <bool COUNT, bool PIN, bool CHK = false, bool SLAB = false>
 __device__ __forceinline__ void trav_record(const DevScene& S, Trav& T, Cnt& cnt, unsigned long long* err = nullptr,
-                                            SlabCnt* sc = nullptr) {
+                                            SlabCnt* sc = nullptr, const RefLds* rl = nullptr) {
     if (T.rk == 0) {
         const int s = __ffs(T.lh) - 1;
         T.lh &= T.lh - 1u;
@@ -1351,7 +1355,8 @@ __device__ __forceinline__ void trav_record(const DevScene& S, Trav& T, Cnt& cnt
     if (T.any ? !(t <= T.tcull) : !(t < T.best.t || (t == T.best.t && key < T.best.key))) return;
     if (T.ref) {
         const uint32_t k0 = (COUNT && sc) ? __popc(T.mask.known) : 0u;
-        const bool reach = leaf_reachable<SLAB>(S, __float_as_int(r3.w), T.o, T.nd, T.mask);
+        const bool reach = (RT_REF_LDS && rl) ? leaf_reachable_lds<SLAB>(S, *rl, __float_as_int(r3.w), T.o, T.nd, T.mask)
+                                              : leaf_reachable<SLAB>(S, __float_as_int(r3.w), T.o, T.nd, T.mask);
         if (COUNT && sc) {
             sc->step = __popc(T.mask.known) - k0;
             sc->slab += sc->step;
@@ -2317,8 +2322,13 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
     __shared__ int coop_pool[COOP_POOL];   // drain lane groups (COOP): node groups of the wave's last queries
     __shared__ int coop_q[CQ_N * COOP_Q];  // ... and those queries
     __shared__ int s_base, s_lim;
+    __shared__ RefLds ref_lds;             // the reference BVH's boxes and leaf paths (candidate culling)
     const int lane_id = threadIdx.x;
     int* stk = stack_lds + lane_id;
+    if (RT_REF_LDS) {
+        ref_lds_load(kernel_params(ka).S, ref_lds, lane_id);
+        __syncthreads();
+    }
     const unsigned long long t_wave0 = (COUNT && kernel_params(ka).wave_trace) ? wall_clock64() : 0ull;
     unsigned int wave_jobs = 0;
     LiteLane L;
@@ -2431,7 +2441,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
             }
             if (tracing) {
                 const bool rec = leaf_pending(T);
-                if (rec) trav_record<COUNT, true, false, true>(S, T, cnt, nullptr, COUNT ? &slab : nullptr);
+                if (rec) trav_record<COUNT, true, false, true>(S, T, cnt, nullptr, COUNT ? &slab : nullptr, &ref_lds);
                 if (COUNT) {  // the wave's ref_slab executions this step: the most any lane did
                     const uint32_t ns = rec ? slab.step : 0u;
                     uint32_t w = 0u;
@@ -2822,8 +2832,10 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_tree_kernel(KPar
     __shared__ int s_base, s_lim;
     __shared__ FanTable ft;
     __shared__ int fan_queue[RT_WAVE];  // lanes waiting for a fan slot, oldest first
+    __shared__ RefLds ref_lds;          // the reference BVH's boxes and leaf paths (candidate culling)
     const int lane_id = threadIdx.x;
     int* stk = stack_lds + lane_id;
+    if (RT_REF_LDS) ref_lds_load(kernel_params(ka).S, ref_lds, lane_id);
     if (lane_id < FAN_SLOTS) ft.owner[lane_id] = -1;
     __syncthreads();
     int fq_head = 0, fq_tail = 0;  // (wave-uniform)
@@ -3059,7 +3071,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_tree_kernel(KPar
             if (tracing) {
                 const bool rec = leaf_pending(T);
                 unsigned long long* err = CHK ? P.stats + RT_STATS_EXTRA + 8 : nullptr;
-                if (rec) trav_record<COUNT, true, CHK, true>(S, T, cnt, err);
+                if (rec) trav_record<COUNT, true, CHK, true>(S, T, cnt, err, nullptr, &ref_lds);
                 const bool nv = T.cur != RT_TRAV_NONE && (!rec || (P.dual && T.lh == 0u));
                 if (nv) trav_node<COUNT, 8, PF, DIRECT, CHK>(S, T, stk, g, cnt, err);
             }
