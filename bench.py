@@ -35,8 +35,16 @@ import numpy as np  # noqa: E402
 
 METRIC = "Mrays/s (primary+shadow+secondary) at 1920×1080; fraction of HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
-# VALU issue peak: 256 CUs x 4 SIMDs x 2.4 GHz / 4 cycles per wave64 VALU instruction
-VALU_PEAK_WAVE_INSTR_S = 256 * 4 * 2.4e9 / 4
+# VALU issue peak: 256 CUs x 4 SIMD-32 units x 2.4 GHz / 2 cycles per wave64 VALU instruction
+# (MI355X_MICROARCH.md: "issues each VALU instruction over 2 cycles (32 lanes/cycle x 2)"; one wave alone
+# on its SIMD needs 4, so the peak takes >= 2 waves interleaving their VALU)
+VALU_PEAK_WAVE_INSTR_S = 256 * 4 * 2.4e9 / 2
+# the SQ counters of the issue / latency picture, one rocprofv3 pass (<= 8 SQ counters per pass)
+SQ_PASS = ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
+           "SQ_BUSY_CYCLES")
+# BASELINE.md's full CPU sample (4 096 pixels of the seed-12345 permutation for C3-C5, whole frames for C1 / C2),
+# timed by tools/cpu_baseline.py on the GPU box's host; the bench line's own leg is a bounded prefix of it
+CPU_FULL = os.path.join("profiles", "r03", "cpu_baseline_full.json")
 BAND_ROWS = 8
 DEFAULT_VIEWS = 64  # frames per step: a 64-view turntable (5.625 deg apart) of the C3 scene in one launch
 # frames per step of the other configs (a step of a few hundred ms at most): C4's 64-sample soft shadows
@@ -113,12 +121,23 @@ def cpu_baseline(config, budget_s=12.0, seed=12345, max_pixels=None):
             legs[key] = {"value": rays / dt / 1e6, "cores": threads, "pixels": npx, "rays": rays,
                          "seconds": round(dt, 2)}
     base = legs["1core_bvh0"]
+    full = None
+    try:  # BASELINE.md's whole sample, timed once in full (tools/cpu_baseline.py) on the GPU box's host
+        with open(os.path.join(REPO, CPU_FULL)) as f:
+            for c in json.load(f)["configs"]:
+                if c["config"] == config:
+                    full = {"file": CPU_FULL, "sample": c["sample"],
+                            "legs": {k: {"Mrays_per_s": v["Mrays_per_s"], "threads": v["threads"], "pixels": v["pixels"],
+                                         "seconds": v["seconds"]} for k, v in c["legs"].items()}}
+    except (OSError, ValueError, KeyError):
+        pass
     return {"value": base["value"], "unit": "Mrays/s", "cores": 1, "kind": "port",
-            "sample": f"first pixels of a seed-{seed} permutation of {config} {W}x{H} (BASELINE.md sample); "
-                      f"{base['pixels']} pixels, {base['rays']} rays in {base['seconds']} s single-threaded, "
-                      f"useBVH=false (reference default); legs: 1 / {allc} threads x useBVH false / true; "
-                      f"host CPU: {_cpu_model()}",
-            "legs": legs}
+            "sample": f"bounded prefix of BASELINE.md's sample (the first pixels of the seed-{seed} permutation of "
+                      f"{config} {W}x{H}): {base['pixels']} pixels, {base['rays']} rays in {base['seconds']} s "
+                      f"single-threaded, useBVH=false (reference default); legs: 1 / {allc} threads x useBVH false / "
+                      f"true; host CPU: {_cpu_model()}; the whole sample (4 096 pixels for C3-C5) timed in full: "
+                      f"full_sample ({CPU_FULL})",
+            "legs": legs, "full_sample": full}
 
 
 def pmc_key(config, views):
@@ -145,18 +164,18 @@ def measure_pmc(config, views, kernel, timeout_s=150):
         return None, "rocprofv3 not found", {}
     med = {}
     with tempfile.TemporaryDirectory(prefix="bench_pmc_") as tmp:
-        for ctr in ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU"):
-            out = os.path.join(tmp, ctr)
-            cmd = ["timeout", "-s", "KILL", str(timeout_s), exe, "--pmc", ctr, "--kernel-trace", "--output-format", "csv",
-                   "-d", out, "-o", "run", "--", sys.executable, os.path.join(REPO, "tools", "prof_target.py"),
+        for group in (("FETCH_SIZE",), ("WRITE_SIZE",), SQ_PASS):
+            out = os.path.join(tmp, group[0])
+            cmd = ["timeout", "-s", "KILL", str(timeout_s), exe, "--pmc", *group, "--kernel-trace", "--output-format",
+                   "csv", "-d", out, "-o", "run", "--", sys.executable, os.path.join(REPO, "tools", "prof_target.py"),
                    config, "2", str(views)]
             r = subprocess.run(cmd, capture_output=True, text=True, cwd=REPO)
             if r.returncode != 0:
-                return None, f"rocprofv3 --pmc {ctr} failed (rc {r.returncode}): {(r.stderr or r.stdout)[-300:]}", med
+                return None, f"rocprofv3 --pmc {' '.join(group)} failed (rc {r.returncode}): {(r.stderr or r.stdout)[-300:]}", med
             kname, m = pmc_summary.collect(out)
-            if ctr not in m or not kname or kernel not in kname:
-                return None, f"rocprofv3 --pmc {ctr}: no counter rows for {kernel}", med
-            med[ctr] = m[ctr]
+            if any(c not in m for c in group) or not kname or kernel not in kname:
+                return None, f"rocprofv3 --pmc {' '.join(group)}: no counter rows for {kernel}", med
+            med.update({c: m[c] for c in group})
     hbm = (2.0 * med["FETCH_SIZE"] + med["WRITE_SIZE"]) * 1024.0
     return hbm, (f"measured in this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over tools/prof_target.py "
                  f"{config} {views} views (the same kernel and library), median per launch; FETCH_SIZE "
@@ -237,6 +256,8 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
+    # the library measured must be the one built from this tree's sources (raises otherwise)
+    prov = R.provenance()
     uv = tuple(int(x) for x in args.dragon_uv.split("x")) if args.dragon_uv else None
     scene, prm, W, H, desc = R.build_config(args.config, dragon_uv=uv)
     if args.resolution:
@@ -342,6 +363,8 @@ def main():
     R.set_counting(True)
     cst = step()
     R.set_counting(False)
+    # lane use of the traversal (counting build): lane node visits / (64 x wave node steps), same for records
+    cdbg = [int(x) for x in ctx.debug_counters()[:7]]
     for _ in range(args.warmup):
         step()
 
@@ -463,23 +486,40 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": (float(pmc) if pmc is not None else None), "traffic_source": pmc_src,
-                         "kernel": kname, "lib_sha": sha, "kernel_avg_ms": avg_ms,
+                         "kernel": kname, "lib_sha": sha, "source_hash": prov["library_source_hash"],
+                         "kernel_avg_ms": avg_ms,
                          "algorithmic_bytes_per_launch": int(bytes0)},
         }
+        lane_use = {"node_steps": cdbg[1] / max(1, 64 * cdbg[4]), "record_steps": cdbg[2] / max(1, 64 * cdbg[5]),
+                    "source": "counting pass of the same kernel (rt_debug_counters): lane visits / (64 x wave steps)"}
         if "SQ_INSTS_VALU" in pmc_med:
-            # the VALU issue roofline beside SURVEY.md §8d's algorithmic-byte one: the kernels are branchy scalar
-            # FP32 whose bytes come mostly from L2 / MALL, so the issue rate is usually the binding limit;
-            # "bound" names whichever fraction is higher (achieved / peak / frac above stay the HBM figures)
+            # the VALU issue roofline beside SURVEY.md §8d's algorithmic-byte one (achieved / peak / frac above stay
+            # the HBM figures of the contract).  The kernels are branchy scalar FP32 whose bytes come mostly from L2 /
+            # MALL, so neither peak binds: "limiter" names what the wave-cycle counters show (waiting on memory vs
+            # issuing) beside the issue fraction against the SIMD-32 peak and the lanes' use of each traversal step
             vi = float(pmc_med["SQ_INSTS_VALU"])
             ia = vi / (avg_ms * 1e-3)
             line["roofline"]["issue"] = {
                 "achieved": ia, "peak": VALU_PEAK_WAVE_INSTR_S, "unit": "wave-instructions/s",
                 "frac": ia / VALU_PEAK_WAVE_INSTR_S, "valu_insts_per_launch": vi,
                 "valu_insts_per_ray": vi / max(1.0, float(cst.rays)),
+                "salu_per_valu": float(pmc_med.get("SQ_INSTS_SALU", 0.0)) / max(1.0, vi),
                 "source": "rocprofv3 --pmc SQ_INSTS_VALU (median per launch, same run) / kernel_avg_ms; peak = 256 CUs "
-                          "x 4 SIMDs x 2.4 GHz / 4 cycles per wave64 VALU instruction"}
-            if ia / VALU_PEAK_WAVE_INSTR_S > achieved / HBM_PEAK_GBS:
-                line["roofline"]["bound"] = "valu-issue"
+                          "x 4 SIMD-32 x 2.4 GHz / 2 cycles per wave64 VALU instruction (MI355X_MICROARCH.md)"}
+            wc = float(pmc_med.get("SQ_WAVE_CYCLES", 0.0))
+            split = ({k: float(pmc_med[k]) / wc for k in ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY")
+                      if k in pmc_med} if wc > 0 else {})
+            issue_frac = ia / VALU_PEAK_WAVE_INSTR_S
+            waiting = split.get("SQ_WAIT_ANY", 0.0)
+            kind = ("memory latency + lane divergence" if waiting > split.get("SQ_ACTIVE_INST_ANY", 1.0)
+                    and issue_frac < 0.7 else "valu-issue" if issue_frac >= 0.7 else "mixed issue / latency")
+            line["roofline"]["limiter"] = {
+                "kind": kind, "issue_frac": issue_frac, "wave_cycles": split, "lane_use": lane_use,
+                "note": "share of wave cycles issuing (SQ_ACTIVE_INST_ANY) / waiting on memory (SQ_WAIT_ANY) / waiting "
+                        "on a dependency (SQ_WAIT_INST_ANY), same rocprofv3 pass; the HBM fraction above is "
+                        "algorithmic bytes (SURVEY.md 8d), most of them served by L2 / MALL (traffic = DRAM bytes)"}
+        else:
+            line["roofline"]["limiter"] = {"lane_use": lane_use}
         if single is not None:
             line["single_frame"] = single
         if world == 1 and not args.no_cpu_baseline:

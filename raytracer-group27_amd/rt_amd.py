@@ -137,7 +137,7 @@ EXPORTS = [
     "rt_philox4x32_10", "rt_debug_wave_trace", "rt_debug_job_trace", "rt_debug_create_ms", "rt_set_build_mode", "rt_debug_build_info", "rt_debug_records", "rt_debug_ref_bvh", "rt_decode_png", "rt_ctx_set_option", "rt_texture_sample",
     "rt_update_lights", "rt_update_materials", "rt_unpermute_views_device", "rt_scene_mesh_count", "rt_scene_mesh_get",
     "rt_ctx_devices", "rt_ctx_peer_stores", "rt_render_views_image_device", "rt_ipc_alloc", "rt_ipc_open", "rt_ipc_close", "rt_device_free",
-    "rt_device_synchronize", "rt_memcpy_dtoh", "rt_debug_slab_check",
+    "rt_device_synchronize", "rt_memcpy_dtoh", "rt_debug_slab_check", "rt_source_hash",
 ]
 IPC_HANDLE_BYTES = 64
 
@@ -229,6 +229,32 @@ def _torch_first():
         torch.cuda.init()
 
 
+def library_source_hash():
+    """rt_source_hash: the source hash compiled into the loaded library (build.py source_hash())."""
+    buf = C.create_string_buffer(32)
+    check(lib().rt_source_hash(buf, 32), "rt_source_hash")
+    return buf.value.decode()
+
+
+def tree_source_hash():
+    """The same hash of this tree's sources (csrc/, include/rt_amd.h, build.py)."""
+    if HERE not in _sys.path:
+        _sys.path.insert(0, HERE)
+    import build as _build
+
+    return _build.source_hash()
+
+
+def provenance(strict=True):
+    """Ties the loaded library to the tree it runs from: {library, tree, match}; raises if they differ and
+    strict (a stale or foreign library must not be measured or tested as this tree's)."""
+    got, want = library_source_hash(), tree_source_hash()
+    if strict and got != want:
+        raise RuntimeError(f"{LIB_PATH} was built from sources {got}, this tree is {want}: rebuild "
+                           "(__graft_entry__.build())")
+    return {"library_source_hash": got, "tree_source_hash": want, "match": got == want}
+
+
 def lib():
     """Load librt_amd.so (raises if it is missing: the product has no fallback)."""
     global _lib
@@ -241,6 +267,7 @@ def lib():
         vp = C.c_void_p
         sigs = {
             "rt_abi_version": ([], C.c_int),
+            "rt_source_hash": ([C.c_char_p, C.c_size_t], C.c_int),
             "rt_device_count": ([C.POINTER(C.c_int)], C.c_int),
             "rt_last_error": ([C.c_char_p, C.c_size_t], C.c_int),
             "rt_scene_new": ([P(vp)], C.c_int),

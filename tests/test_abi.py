@@ -40,6 +40,16 @@ def test_abi_version_and_struct_sizes(R):
     assert ctypes.sizeof(R.rt_texture) == 24
 
 
+def test_library_built_from_this_tree(R):
+    """Provenance: the source hash compiled into the library (rt_source_hash) is the hash of this tree's
+    sources (build.py source_hash), and the file stamp build.py reads agrees with the C-ABI call."""
+    import build
+
+    p = R.provenance(strict=False)
+    assert p["match"], p
+    assert build.library_hash(R.LIB_PATH) == p["library_source_hash"]
+
+
 def test_library_reads_no_environment(R):
     """Render paths are chosen by the scene and explicit context options (rt_ctx_set_option), never
     by environment variables: the library imports no getenv / secure_getenv."""

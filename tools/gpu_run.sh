@@ -17,6 +17,7 @@
 #   wave[:CFG[:VIEWS[:COUNT]]]  tools/wave_trace.py (per-wave start / drain / end; COUNT 1: counting build)
 #   jobs[:CFG[:OPTS]]           tools/job_trace.py (per-pixel query chains of a single frame; OPTS k=v;k=v)
 #   ranks                       bench.py N = 2 on this one GPU (gloo control plane, IPC exchange)
+#   ipc[:VIEWS]                 tools/ipc_probe.py: owner + opener of an IPC image buffer, each step timestamped
 #   cpu_baseline                tools/cpu_baseline.py (BASELINE.md's full CPU samples on the host)
 #   times                       tools/time_configs.py (every config, single frame and batch)
 set -o pipefail
@@ -51,6 +52,7 @@ for step in "$@"; do
     wave)  run 300 wave_${TAG}${c:+_count}.log env WT_VIEWS=${b:-1} WT_COUNT=${c:-0} python tools/wave_trace.py ${a:-C3} ;;
     jobs)  run 300 jobs_${TAG}${b:+_$b}.log python tools/job_trace.py ${a:-C3} ${b//;/ } ;;
     ranks) run 600 ranks_${TAG}.json env BENCH_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29555 bench.py --gpus 2 --steps 5 --warmup 1 --no-single-frame ;;
+    ipc)   run 150 ipc_${TAG}_v${a:-96}.log python -u tools/ipc_probe.py --views ${a:-96} --timeout 110 ;;
     cpu_baseline) run 1500 cpu_baseline_${TAG}.json python tools/cpu_baseline.py --out gpurun_out/cpu_baseline_${TAG}.out.json ;;
     times) run 900 times_${TAG}.log python tools/time_configs.py ;;
     *) echo "unknown step $step"; exit 2 ;;
