@@ -28,6 +28,7 @@
 #include "rt_internal.h"
 #include "rt_kernels.hip"
 #include "rt_megakernel.hip"
+#include "rt_wavefront.hip"
 
 using namespace rt;
 
@@ -162,6 +163,11 @@ struct rt_ctx {
     size_t bands_bytes = 0;
     std::vector<float*> stage;        // devices[0] (primary context only): replica i's band copy
     std::vector<size_t> stage_bytes;
+    // wavefront path (rt_wavefront.hip): its counters, path-ray results, queues and shading points
+    int opt_wavefront = -1;
+    float* d_wf = nullptr;   // one allocation, carved by wf_layout
+    size_t wf_bytes = 0;
+    int wf_trace_blocks[2] = {0, 0};  // resident blocks of the trace kernel (plain, counting)
 };
 
 // device ranges this library opened from other processes (rt_ipc_open): mapped for the opening device only
@@ -282,6 +288,7 @@ extern "C" int rt_destroy(rt_ctx* c) {
     if (c->d_views) hipFree(c->d_views);
     if (c->d_frames) hipFree(c->d_frames);
     if (c->d_plane_tab) hipFree(c->d_plane_tab);
+    if (c->d_wf) hipFree(c->d_wf);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
     return RT_OK;
@@ -967,6 +974,10 @@ static int set_option_one(rt_ctx* c, int option, int value) {
             if (value < 0 || value > 65535) break;
             c->opt_il_tail = value;
             return RT_OK;
+        case RT_OPT_WAVEFRONT:
+            if (value < -1 || value > 32) break;
+            c->opt_wavefront = value;
+            return RT_OK;
         default:
             set_error("rt_ctx_set_option: unknown option");
             return RT_ERR_INVALID;
@@ -1359,11 +1370,123 @@ static void shape_options(const rt_ctx* c, KParams& K) {
     K.dual = c->opt_dual >= 0 ? c->opt_dual : 1;
 }
 
+// ---- the wavefront path (rt_wavefront.hip) ----
+// its scope: the opaque kernel's renders with one camera sample per pixel and at most 32 lights (one bit each)
+#define RT_WF_REFILL 16             // trace kernel: waiting lanes that take new queries together (RT_OPT_WAVEFRONT 2..32)
+#define RT_WF_BUDGET (24ull << 30)  // bytes of queues and shading points per chunk of camera jobs (at most)
+static bool wf_path(const rt_ctx* c, const KParams& K) {
+    if (c->opt_wavefront == 0 || !opaque_path(c, K, true) || K.aa || K.multi) return false;
+    if (K.S.npl + K.S.nspot > 32) return false;
+    return c->opt_wavefront > 0;
+}
+
+static int wf_trace_grid(rt_ctx* c, bool count) {
+    int& g = c->wf_trace_blocks[count ? 1 : 0];
+    if (g > 0) return g;
+    int cus = 0, per_cu = 0;
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
+    const hipError_t e = count ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wf_trace_kernel<true, false>, 64, 0)
+                               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wf_trace_kernel<false, false>, 64, 0);
+    if (e != hipSuccess || per_cu <= 0) per_cu = 8;
+    g = std::max(1, cus) * per_cu;
+    return g;
+}
+
+// A render as the wavefront of rt_wavefront.hip: the camera jobs in chunks whose worst-case queues fit
+// RT_WF_BUDGET (every path ray may hit, every shading point may need a segment per light), per chunk
+// T_0 S_0 T_1 S_1 ... T_{L+1} S_{L+1} (L = max_reflection_level) on the caller's stream.
+template <bool COUNT>
+static int launch_wavefront(rt_ctx* c, KParams& K, hipStream_t st, rt_stats* stats) {
+    const long long tiles_x = (K.W + 7) / 8, tiles_y = (K.band_rows + 7) / 8;
+    const long long view_jobs = tiles_x * tiles_y * K.n_local_bands * 64;
+    const long long njobs = view_jobs * std::max(1, K.n_views);
+    const long long pix_max = (long long)std::max(1, K.n_views) * (K.out_image ? K.H : K.view_rows) * K.W;
+    if (njobs > 0x7FFFFFFFll || pix_max >= (1ll << 32)) {
+        set_error("wavefront render: batch too large (job or pixel index overflows)");
+        return RT_ERR_INVALID;
+    }
+    K.view_jobs = (int)view_jobs;
+    K.interleave = 0;
+    K.interleave_view = 0;
+    K.centre_first = 0;
+    K.refill = c->opt_wavefront >= 2 ? c->opt_wavefront : RT_WF_REFILL;
+    HIP_TRY(hipMemsetAsync(c->d_stats, 0, RT_STATS_BYTES, st));
+    const int nl = std::max(1, K.S.npl + K.S.nspot);
+    const size_t per_job = sizeof(int2) + 2 * 48 + 32 * (size_t)nl + 2 * 64;
+    size_t budget = RT_WF_BUDGET, free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) budget = std::min(budget, (size_t)(free_b / 2));
+    long long J = std::min<long long>(njobs, std::max<long long>(64, (long long)(budget / per_job)));
+    J = (J + 63) / 64 * 64;
+    const size_t cnt_bytes = (sizeof(WfCnt) + 255) & ~(size_t)255;
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t b_res = al(J * sizeof(int2)), b_qp = al(J * 48), b_qs = al(J * 32 * (size_t)nl), b_nd = al(J * 64);
+    const size_t need = cnt_bytes + b_res + 2 * b_qp + b_qs + 2 * b_nd;
+    int rc = ensure(c, &c->d_wf, &c->wf_bytes, need);
+    if (rc != RT_OK) return rc;
+    char* base = reinterpret_cast<char*>(c->d_wf);
+    WfBufs B{};
+    B.cnt = reinterpret_cast<WfCnt*>(base);
+    base += cnt_bytes;
+    B.res = reinterpret_cast<int2*>(base);
+    base += b_res;
+    B.qp[0] = reinterpret_cast<float4*>(base);
+    base += b_qp;
+    B.qp[1] = reinterpret_cast<float4*>(base);
+    base += b_qp;
+    B.qs = reinterpret_cast<float4*>(base);
+    base += b_qs;
+    B.nodes[0] = reinterpret_cast<float4*>(base);
+    base += b_nd;
+    B.nodes[1] = reinterpret_cast<float4*>(base);
+    B.nl = K.S.npl + K.S.nspot;
+    const int tgrid = wf_trace_grid(c, COUNT);
+    int cus = 0;
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
+    const int sgrid = std::max(1, cus) * 8;
+    HIP_TRY(hipEventRecord(c->ev0, st));
+    for (long long g0 = 0; g0 < njobs; g0 += J) {
+        B.job0 = (int)g0;
+        B.njobs = (int)std::min<long long>(J, njobs - g0);
+        HIP_TRY(hipMemsetAsync(B.cnt, 0, sizeof(WfCnt), st));
+        for (int l = 0; l <= K.max_level + 1; ++l) {
+            B.level = l;
+            if (l == 0)
+                hipLaunchKernelGGL((wf_trace_kernel<COUNT, true>), dim3(tgrid), dim3(64), 0, st, K, B);
+            else
+                hipLaunchKernelGGL((wf_trace_kernel<COUNT, false>), dim3(tgrid), dim3(64), 0, st, K, B);
+            hipLaunchKernelGGL((wf_shade_kernel<COUNT>), dim3(sgrid), dim3(256), 0, st, K, B);
+        }
+    }
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(c->ev1, st));
+    std::snprintf(c->last_kernel, sizeof(c->last_kernel), "rt::wf_trace_kernel<%s", COUNT ? "true" : "false");
+    if (stats) {
+        unsigned long long h[13] = {0};
+        HIP_TRY(hipMemcpyAsync(h, c->d_stats, sizeof(h), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        std::memset(stats, 0, sizeof(*stats));
+        stats->rays = h[0];
+        stats->node_visits = h[1];
+        stats->tri_tests = h[2];
+        stats->hits = h[3];
+        stats->ub_hits = h[12];
+        float ms = 0.0f;
+        HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+        stats->kernel_ms = ms;
+        stats->node_bytes = 128u;
+        std::memcpy(stats->kernel, c->last_kernel, sizeof(stats->kernel));
+        stats->kernel[sizeof(stats->kernel) - 1] = 0;
+    }
+    return RT_OK;
+}
+
 static int launch_render(rt_ctx* c, KParams& K, hipStream_t st, int count_mode, rt_stats* stats) {
     const int tiles_x = (K.W + 7) / 8;
     const int tiles_y = (K.band_rows + 7) / 8;
     const long long blocks = (long long)tiles_x * tiles_y * K.n_local_bands;
     shape_options(c, K);
+    if (blocks > 0 && wf_path(c, K))
+        return count_mode ? launch_wavefront<true>(c, K, st, stats) : launch_wavefront<false>(c, K, st, stats);
     HIP_TRY(hipMemsetAsync(c->d_stats, 0, RT_STATS_BYTES, st));
     if (blocks > 0) {
         JobSrc J{};

@@ -7,7 +7,7 @@ import contextlib
 def defaults(R):
     return {R.OPT_KERNEL: R.KERNEL_AUTO, R.OPT_VARIANT: -1, R.OPT_COOP: -1, R.OPT_COOP_MAX: 0, R.OPT_REFILL: 0,
             R.OPT_FAN: 1, R.OPT_INTERLEAVE: -1, R.OPT_FAN_CAP: 0, R.OPT_DUAL_STEP: -1, R.OPT_OPAQUE: -1,
-            R.OPT_CENTRE_FIRST: -1, R.OPT_TREE: -1, R.OPT_INTERLEAVE_TAIL: 0}
+            R.OPT_CENTRE_FIRST: -1, R.OPT_TREE: -1, R.OPT_INTERLEAVE_TAIL: 0, R.OPT_WAVEFRONT: -1}
 
 
 def kernel_classes(R):
@@ -42,6 +42,10 @@ def all_variants(R):
         {R.OPT_KERNEL: df, R.OPT_TREE: 0},                      # general kernels where the tree kernel is eligible
         {R.OPT_KERNEL: df, R.OPT_TREE: 1},                      # the tree kernel with the re-visit group stack
         {R.OPT_KERNEL: df, R.OPT_TREE: 2},                      # ... and with the direct one (its default)
+        {R.OPT_KERNEL: df, R.OPT_WAVEFRONT: 0},                 # the opaque megakernel where the wavefront is eligible
+        {R.OPT_KERNEL: df, R.OPT_WAVEFRONT: 1},                 # the wavefront path (trace / shade kernels)
+        {R.OPT_KERNEL: df, R.OPT_WAVEFRONT: 2},                 # ... its trace kernel refilling at 2 waiting lanes
+        {R.OPT_KERNEL: df, R.OPT_WAVEFRONT: 32},                # ... and at 32
     ]
     return out
 
