@@ -975,7 +975,7 @@ static int set_option_one(rt_ctx* c, int option, int value) {
             c->opt_il_tail = value;
             return RT_OK;
         case RT_OPT_WAVEFRONT:
-            if (value < -1 || value > 32) break;
+            if (value < -1 || value > 64) break;
             c->opt_wavefront = value;
             return RT_OK;
         default:

@@ -75,6 +75,7 @@ __device__ __forceinline__ void wf_light(const DevScene& S, int li, v3& lp, v3& 
 #ifndef RT_WF_WAVES
 #define RT_WF_WAVES 5
 #endif
+#define RT_WF_CHUNK 64  // queries a wave reserves per queue-head atomic
 template <bool COUNT, bool PRIMARY>
 __global__ __launch_bounds__(64, RT_WF_WAVES) void wf_trace_kernel(KParams, WfBufs) {
     const void* ka = (const void*)__builtin_amdgcn_kernarg_segment_ptr();
@@ -82,10 +83,6 @@ __global__ __launch_bounds__(64, RT_WF_WAVES) void wf_trace_kernel(KParams, WfBu
     __shared__ RefLds ref_lds;
     const int lane_id = threadIdx.x;
     int* stk = stack_lds + lane_id;
-    if (RT_REF_LDS) {
-        ref_lds_load(kernel_params(ka).S, ref_lds, lane_id);
-        __syncthreads();
-    }
     // the level's work: n_path path rays (camera jobs at l = 0), then n_seg cansee segments
     int n_path, n_seg, level;
     {
@@ -95,6 +92,13 @@ __global__ __launch_bounds__(64, RT_WF_WAVES) void wf_trace_kernel(KParams, WfBu
         n_seg = PRIMARY ? 0 : B.cnt->qs[level];
     }
     const int n_all = n_path + n_seg;
+    // a level with few queries runs on as many waves as give each lane one (the others leave at once: no
+    // atomics on the queue heads, no reference-BVH load)
+    if ((int)blockIdx.x >= ((n_all + 63) >> 6) + 8) return;
+    if (RT_REF_LDS) {
+        ref_lds_load(kernel_params(ka).S, ref_lds, lane_id);
+        __syncthreads();
+    }
     Trav T;
     trav_idle(T);
     Cnt cnt{};
@@ -102,28 +106,40 @@ __global__ __launch_bounds__(64, RT_WF_WAVES) void wf_trace_kernel(KParams, WfBu
     uint32_t tag = 0u;           // a segment's shading point << 5 | light
     bool tracing = false, done = false;
     int xr = (int)(blockIdx.x & 7), xtried = 0;
+    // the wave's reserved block of queries [nxt, end) (wave-uniform): one queue-head atomic per RT_WF_CHUNK
+    int nxt = 0, end = 0;
     for (;;) {
         const KParams& P = *(const KParams*)fresh_kernarg(ka);
         const DevScene& S = P.S;
-        // ---- refill: the waiting lanes take the next queries of the wave's range ----
+        // ---- refill: the waiting lanes take the next queries, from the wave's block, then new blocks ----
         {
             const bool idle = !tracing && !done;
             const unsigned long long want = __ballot(idle);
             const int nwant = __popcll(want);
             if (want && (nwant >= P.refill || !__any(tracing))) {
                 const WfBufs& B = wf_bufs(ka);
-                // range x of the level's work: [x * n_all / 8, (x + 1) * n_all / 8)
-                const int lo = (int)(((long long)xr * n_all) >> 3), hi = (int)(((long long)(xr + 1) * n_all) >> 3);
-                int base = 0;
-                if (lane_id == __ffsll((long long)want) - 1) base = lo + atomicAdd(&B.cnt->head[level][32 * xr], nwant);
-                base = __shfl(base, __ffsll((long long)want) - 1);
-                if (base + nwant >= hi) {  // the range is used up: the next one
-                    xr = (xr + 1) & 7;
-                    ++xtried;
+                const int rank = __popcll(want & ((1ull << lane_id) - 1ull)), leader = __ffsll((long long)want) - 1;
+                int k = -1, served = 0;
+                for (;;) {  // wave-uniform
+                    const int take = min(nwant - served, end - nxt);
+                    if (idle && rank >= served && rank < served + take) k = nxt + (rank - served);
+                    nxt += take;
+                    served += take;
+                    if (served == nwant || xtried >= 8) break;
+                    // the next block of range xr: [xr * n_all / 8, (xr + 1) * n_all / 8)
+                    const int lo = (int)(((long long)xr * n_all) >> 3), hi = (int)(((long long)(xr + 1) * n_all) >> 3);
+                    int b = 0;
+                    if (lane_id == leader) b = lo + atomicAdd(&B.cnt->head[level][32 * xr], RT_WF_CHUNK);
+                    b = __shfl(b, leader);
+                    if (b + RT_WF_CHUNK >= hi) {  // the range is used up with this block: the next one after it
+                        xr = (xr + 1) & 7;
+                        ++xtried;
+                    }
+                    nxt = min(b, hi);
+                    end = min(b + RT_WF_CHUNK, hi);
                 }
                 if (idle) {
-                    const int k = base + __popcll(want & ((1ull << lane_id) - 1ull));
-                    if (k < hi) {
+                    if (k >= 0) {
                         v3 o, d;
                         float t0 = FLT_MAX, sdist = 0.0f;
                         bool seg = false;

@@ -2,7 +2,7 @@
 times: one frame (views = 1) or a turntable batch of V views in one launch (bench.py --views V), every pixel
 stored in its setPixel place (rt_render_views_image_device).
 
-    python tools/prof_target.py CONFIG N [VIEWS]
+    python tools/prof_target.py CONFIG N [VIEWS]      (PT_OPTS="16=1" selects render-path options)
 """
 import os, sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -13,6 +13,10 @@ n = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 views = int(sys.argv[3]) if len(sys.argv) > 3 else 1
 s, p, W, H, desc = R.build_config(cfg)
 ctx = R.Context(s)
+# PT_OPTS="k=v,k=v": rt_ctx_set_option settings (developer A/B of render paths under the profiler)
+for kv in filter(None, os.environ.get("PT_OPTS", "").split(",")):
+    k, v = kv.split("=")
+    ctx.set_option(int(k), int(v))
 if views == 1:
     cam = R.camera_from_trackball(aspect=R.aspect_of(W, H))
     for _ in range(n):
