@@ -11,6 +11,8 @@
 #   bench[:CFG[:VIEWS]]         bench.py line (N = 1; roofline.traffic measured by its rocprofv3 passes)
 #   stats[:CFG[:VIEWS]]         rocprofv3 --kernel-trace --stats of bench.py (kernel summary for profiles/)
 #   kstats:CFG:VIEWS:OPTS:TAG2  rocprofv3 --kernel-trace --stats of tools/prof_target.py (OPTS k=v;k=v render options)
+#   pmcx:CFG:VIEWS:OPTS:TAG2:CTRS  one rocprofv3 --pmc pass (CTRS ;-separated) of tools/prof_target.py (OPTS k=v;k=v),
+#                               summed per kernel (tools/pmc_by_kernel.py)
 #   pmc[:CFG[:VIEWS]]           the PMC counter groups of tools/pmc_counters.txt (tools/profile.sh)
 #   ab:CFGS:VIEWS:ROUNDS[:ARMS] tools/ab_variants.py (CFGS / ARMS comma-separated; ARMS name=k=v;k=v)
 #   simd[:CFG[:VIEWS[:ARMS]]]   tools/simd_eff.py (counting build: lanes per node / record step; ARMS comma-separated
@@ -48,6 +50,9 @@ for step in "$@"; do
            find gpurun_out/stats_${TAG}_${a:-C3} -name "*kernel_stats.csv" -exec head -3 {} \; ;;
     kstats) run 300 kstats_${TAG}_${d:-x}.log env PT_OPTS="${c//;/,}" rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/kstats_${TAG}_${d:-x} -o run -- python3 tools/prof_target.py ${a:-C3} 3 ${b:-64}
            find gpurun_out/kstats_${TAG}_${d:-x} -name "*kernel_stats.csv" -exec cat {} \; ;;
+    pmcx)  IFS=: read -r _n _a _b _c _d CTRS <<< "$step"
+           run 120 pmcx_${TAG}_${d:-x}.log env PT_OPTS="${c//;/,}" timeout -s KILL 100 rocprofv3 --pmc ${CTRS//;/ } --kernel-trace --output-format csv -d gpurun_out/pmcx_${TAG}_${d:-x} -o run -- python3 tools/prof_target.py ${a:-C3} 2 ${b:-64}
+           python3 tools/pmc_by_kernel.py gpurun_out/pmcx_${TAG}_${d:-x} 2 | tee gpurun_out/pmcx_${TAG}_${d:-x}.txt | cut -c1-400 ;;
     pmc)   run 900 pmc_${TAG}_${a:-C3}.log bash tools/profile.sh ${TAG}_${a:-C3} ${a:-C3} ${b:-64} ;;
     ab)    ARMS=(); if [ -n "$d" ]; then for x in ${d//,/ }; do ARMS+=("${x//;/,}"); done; ARMS=(--arms "${ARMS[@]/=/:}"); fi
            run 900 ab_${TAG}.log python -u tools/ab_variants.py ${a//,/ } --views ${b:-16} --rounds ${c:-3} "${ARMS[@]}" ;;
