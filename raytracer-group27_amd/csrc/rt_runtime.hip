@@ -1373,7 +1373,8 @@ static void shape_options(const rt_ctx* c, KParams& K) {
 // ---- the wavefront path (rt_wavefront.hip) ----
 // its scope: the opaque kernel's renders with one camera sample per pixel and at most 32 lights (one bit each)
 #define RT_WF_REFILL 16             // trace kernel: waiting lanes that take new queries together (RT_OPT_WAVEFRONT 2..32)
-#define RT_WF_BUDGET (24ull << 30)  // bytes of queues and shading points per chunk of camera jobs (at most)
+#define RT_WF_BUDGET (64ull << 30)  // bytes of queues and shading points per chunk of camera jobs (at most; and
+                                    // at most a third of the free HBM)
 static bool wf_path(const rt_ctx* c, const KParams& K) {
     if (c->opt_wavefront == 0 || !opaque_path(c, K, true) || K.aa || K.multi) return false;
     if (K.S.npl + K.S.nspot > 32) return false;
@@ -1412,32 +1413,37 @@ static int launch_wavefront(rt_ctx* c, KParams& K, hipStream_t st, rt_stats* sta
     K.refill = c->opt_wavefront >= 2 ? c->opt_wavefront : RT_WF_REFILL;
     HIP_TRY(hipMemsetAsync(c->d_stats, 0, RT_STATS_BYTES, st));
     const int nl = std::max(1, K.S.npl + K.S.nspot);
-    const size_t per_job = sizeof(int2) + 2 * 48 + 32 * (size_t)nl + 2 * 64;
+    // per camera job of a chunk: two hit lists (16 B), two path-ray queues (80 B), the segment queue (64 B per
+    // light) and two shading-point arrays (64 B) -- every path ray may hit
+    const size_t per_job = 2 * sizeof(int4) + 2 * 80 + 64 * (size_t)nl + 2 * 64;
     size_t budget = RT_WF_BUDGET, free_b = 0, total_b = 0;
-    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) budget = std::min(budget, (size_t)(free_b / 2));
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) budget = std::min(budget, (size_t)(free_b / 3));
     long long J = std::min<long long>(njobs, std::max<long long>(64, (long long)(budget / per_job)));
     J = (J + 63) / 64 * 64;
     const size_t cnt_bytes = (sizeof(WfCnt) + 255) & ~(size_t)255;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    const size_t b_res = al(J * sizeof(int2)), b_qp = al(J * 48), b_qs = al(J * 32 * (size_t)nl), b_nd = al(J * 64);
-    const size_t need = cnt_bytes + b_res + 2 * b_qp + b_qs + 2 * b_nd;
+    const size_t b_hit = al(J * sizeof(int4)), b_qp = al(J * 80), b_qs = al(J * 64 * (size_t)nl), b_nd = al(J * 64);
+    const size_t need = cnt_bytes + 2 * b_hit + 2 * b_qp + b_qs + 2 * b_nd;
     int rc = ensure(c, &c->d_wf, &c->wf_bytes, need);
     if (rc != RT_OK) return rc;
     char* base = reinterpret_cast<char*>(c->d_wf);
     WfBufs B{};
     B.cnt = reinterpret_cast<WfCnt*>(base);
     base += cnt_bytes;
-    B.res = reinterpret_cast<int2*>(base);
-    base += b_res;
-    B.qp[0] = reinterpret_cast<float4*>(base);
-    base += b_qp;
-    B.qp[1] = reinterpret_cast<float4*>(base);
-    base += b_qp;
+    for (int k = 0; k < 2; ++k) {
+        B.hit[k] = reinterpret_cast<int4*>(base);
+        base += b_hit;
+    }
+    for (int k = 0; k < 2; ++k) {
+        B.qp[k] = reinterpret_cast<float4*>(base);
+        base += b_qp;
+    }
     B.qs = reinterpret_cast<float4*>(base);
     base += b_qs;
-    B.nodes[0] = reinterpret_cast<float4*>(base);
-    base += b_nd;
-    B.nodes[1] = reinterpret_cast<float4*>(base);
+    for (int k = 0; k < 2; ++k) {
+        B.nodes[k] = reinterpret_cast<float4*>(base);
+        base += b_nd;
+    }
     B.nl = K.S.npl + K.S.nspot;
     const int tgrid = wf_trace_grid(c, COUNT);
     int cus = 0;
