@@ -374,7 +374,8 @@ int rt_set_counting(int on);
  * [16..18] node re-visits of popped stack groups, their slots, their slots still hit; [19] / [20] the opaque
  * kernel's reference-box tests of candidate culling per lane / per wave step, [21..23] its lane iterations held to a
  * record test with a node to visit, with both a node visit and a record test, and in all; [24] / [25] the first
- * out-of-range index of a checked build (code << 32 | value) and their count). */
+ * out-of-range index of a checked build (code << 32 | value) and their count; [32..49] the last wavefront render's
+ * path-ray hits per recursion level, of its last chunk of camera jobs). */
 int rt_debug_counters(rt_ctx* ctx, uint64_t* out, int n);
 /* Context options: test and developer hooks (the library reads no environment variables).  The
  * defaults are the shipped path; every setting renders the same image and ray count. */

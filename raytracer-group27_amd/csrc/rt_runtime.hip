@@ -2029,6 +2029,11 @@ extern "C" int rt_debug_counters(rt_ctx* c, uint64_t* out, int n) {
     unsigned long long h[RT_STATS_EXTRA + 16] = {0};
     HIP_TRY(hipMemcpy(h, c->d_stats, sizeof(h), hipMemcpyDeviceToHost));
     for (int i = 0; i < n && i < 32; ++i) out[i] = h[i < 16 ? i : RT_STATS_EXTRA + i - 16];
+    if (n > 32 && c->d_wf) {  // [32 ..]: the last wavefront chunk's hits per level (WfCnt::hits)
+        int wh[RT_MAX_DEPTH + 2] = {0};
+        HIP_TRY(hipMemcpy(wh, c->d_wf, sizeof(wh), hipMemcpyDeviceToHost));
+        for (int i = 32; i < n && i < 32 + RT_MAX_DEPTH + 2; ++i) out[i] = (uint64_t)wh[i - 32];
+    }
     return RT_OK;
 }
 

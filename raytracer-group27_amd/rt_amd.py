@@ -696,9 +696,9 @@ class Context:
         check(lib().rt_update_materials(self.h, len(mesh_materials), mm, len(sphere_materials), sm),
               "rt_update_materials")
 
-    def debug_counters(self):
-        out = np.zeros(32, np.uint64)
-        check(lib().rt_debug_counters(self.h, out.ctypes.data_as(C.POINTER(C.c_uint64)), 32))
+    def debug_counters(self, n=32):
+        out = np.zeros(n, np.uint64)
+        check(lib().rt_debug_counters(self.h, out.ctypes.data_as(C.POINTER(C.c_uint64)), n))
         return out
 
     def selftest_math(self, x, y):
