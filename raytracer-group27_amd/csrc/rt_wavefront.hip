@@ -149,7 +149,7 @@ __global__ __launch_bounds__(64, RT_WF_WAVES) void wf_trace_kernel(KParams, WfBu
     bool tracing = false, done = false;
     int xr = (int)(blockIdx.x & 7), xtried = 0;
     // the wave's reserved block [nxt, end) (wave-uniform); camera jobs: the block is one tile, decoded once
-    int nxt = 0, end = 0;
+    int nxt = 0, end = 0, bstart = 0;
     int t_view = 0, t_px0 = 0, t_py0 = 0, t_rib0 = 0, t_row0 = 0, t_lb = 0;
     int hpos = 0;                   // entries in hst (wave-uniform)
     const int ntiles = n_all >> 6;  // camera jobs: whole tiles (view_jobs and job0 are multiples of 64)
@@ -183,6 +183,7 @@ __global__ __launch_bounds__(64, RT_WF_WAVES) void wf_trace_kernel(KParams, WfBu
                     }
                     nxt = min(b, hi);
                     end = min(b + RT_WF_BLOCK, hi);
+                    bstart = nxt;
                     if (PRIMARY && nxt < end) {
                         // the tile's pixel 0 (job_pixel's decode, once per tile)
                         uint32_t rpix;
@@ -204,7 +205,7 @@ __global__ __launch_bounds__(64, RT_WF_WAVES) void wf_trace_kernel(KParams, WfBu
                 const int take = min(nwant, end - nxt);
                 const int rank = __popcll(want & ((1ull << lane_id) - 1ull));
                 const int k = (idle && rank < take) ? nxt + rank : -1;
-                const int j = k - nxt;  // camera jobs: the pixel of the tile
+                const int j = k - bstart;  // camera jobs: the pixel of the tile (a block is served over several refills)
                 nxt += take;
                 if (idle) {
                     if (k >= 0) {
