@@ -167,7 +167,8 @@ struct rt_ctx {
     int opt_wavefront = -1;
     float* d_wf = nullptr;   // one allocation, carved by wf_layout
     size_t wf_bytes = 0;
-    int wf_trace_blocks[2] = {0, 0};  // resident blocks of the trace kernel (plain, counting)
+    int wf_trace_blocks[8] = {0};  // resident blocks of the trace kernel's builds (plain, counting)
+    int opt_wf_build = 0;          // RT_OPT_WF_BUILD
 };
 
 // device ranges this library opened from other processes (rt_ipc_open): mapped for the opening device only
@@ -978,6 +979,10 @@ static int set_option_one(rt_ctx* c, int option, int value) {
             if (value < -1 || value > 64) break;
             c->opt_wavefront = value;
             return RT_OK;
+        case RT_OPT_WF_BUILD:
+            if (value < 0 || value > 3) break;
+            c->opt_wf_build = value;
+            return RT_OK;
         default:
             set_error("rt_ctx_set_option: unknown option");
             return RT_ERR_INVALID;
@@ -1381,16 +1386,33 @@ static bool wf_path(const rt_ctx* c, const KParams& K) {
     return c->opt_wavefront > 0;
 }
 
-static int wf_trace_grid(rt_ctx* c, bool count) {
-    int& g = c->wf_trace_blocks[count ? 1 : 0];
+// the trace kernel's builds (RT_OPT_WF_BUILD): 5 waves per SIMD (default), 6, 4 with the node prefetch, 8
+static const int kWfBuilds[4] = {RT_WF_W5, 6, 4 | RT_WF_PF, 8};
+template <bool COUNT, int WV>
+static int wf_occupancy(int* per_cu) {
+    return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, wf_trace_kernel<COUNT, false, WV>, 64, 0);
+}
+static int wf_trace_grid(rt_ctx* c, bool count, int build) {
+    int& g = c->wf_trace_blocks[count ? 4 + build : build];
     if (g > 0) return g;
     int cus = 0, per_cu = 0;
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
-    const hipError_t e = count ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wf_trace_kernel<true, false>, 64, 0)
-                               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wf_trace_kernel<false, false>, 64, 0);
-    if (e != hipSuccess || per_cu <= 0) per_cu = 8;
+    int e = 1;
+    if (count) e = wf_occupancy<true, RT_WF_W5>(&per_cu);
+    else if (build == 1) e = wf_occupancy<false, 6>(&per_cu);
+    else if (build == 2) e = wf_occupancy<false, 4 | RT_WF_PF>(&per_cu);
+    else if (build == 3) e = wf_occupancy<false, 8>(&per_cu);
+    else e = wf_occupancy<false, RT_WF_W5>(&per_cu);
+    if (e != 0 || per_cu <= 0) per_cu = 8;
     g = std::max(1, cus) * per_cu;
     return g;
+}
+template <bool COUNT, bool PRIMARY>
+static void wf_launch_trace(int build, int grid, hipStream_t st, const KParams& K, const WfBufs& B) {
+    if (COUNT || build == 0) hipLaunchKernelGGL((wf_trace_kernel<COUNT, PRIMARY, RT_WF_W5>), dim3(grid), dim3(64), 0, st, K, B);
+    else if (build == 1) hipLaunchKernelGGL((wf_trace_kernel<false, PRIMARY, 6>), dim3(grid), dim3(64), 0, st, K, B);
+    else if (build == 2) hipLaunchKernelGGL((wf_trace_kernel<false, PRIMARY, 4 | RT_WF_PF>), dim3(grid), dim3(64), 0, st, K, B);
+    else hipLaunchKernelGGL((wf_trace_kernel<false, PRIMARY, 8>), dim3(grid), dim3(64), 0, st, K, B);
 }
 
 // A render as the wavefront of rt_wavefront.hip: the camera jobs in chunks whose worst-case queues fit
@@ -1445,7 +1467,8 @@ static int launch_wavefront(rt_ctx* c, KParams& K, hipStream_t st, rt_stats* sta
         base += b_nd;
     }
     B.nl = K.S.npl + K.S.nspot;
-    const int tgrid = wf_trace_grid(c, COUNT);
+    const int build = COUNT ? 0 : c->opt_wf_build;
+    const int tgrid = wf_trace_grid(c, COUNT, build);
     int cus = 0;
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
     const int sgrid = std::max(1, cus) * 8;
@@ -1457,9 +1480,9 @@ static int launch_wavefront(rt_ctx* c, KParams& K, hipStream_t st, rt_stats* sta
         for (int l = 0; l <= K.max_level + 1; ++l) {
             B.level = l;
             if (l == 0)
-                hipLaunchKernelGGL((wf_trace_kernel<COUNT, true>), dim3(tgrid), dim3(64), 0, st, K, B);
+                wf_launch_trace<COUNT, true>(build, tgrid, st, K, B);
             else
-                hipLaunchKernelGGL((wf_trace_kernel<COUNT, false>), dim3(tgrid), dim3(64), 0, st, K, B);
+                wf_launch_trace<COUNT, false>(build, tgrid, st, K, B);
             hipLaunchKernelGGL((wf_shade_kernel<COUNT>), dim3(sgrid), dim3(256), 0, st, K, B);
         }
     }

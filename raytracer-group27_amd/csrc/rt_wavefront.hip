@@ -111,12 +111,13 @@ __device__ __forceinline__ void wf_init(bool use_bvh, bool shadow, bool all_opaq
 // the wave's block at the next refill (once `refill` lanes wait, or none traces).  The traversal step is the
 // opaque kernel's (dual record + node visit, the direct group stack in LDS, the reference BVH in LDS for
 // the culling).  Path hits go through a 64-entry LDS buffer to the level's hit list (one atomic per 64).
-#ifndef RT_WF_WAVES
-#define RT_WF_WAVES 5
-#endif
 #define RT_WF_BLOCK 64  // queries a wave reserves per queue-head atomic (camera jobs: one 8x8 tile)
-template <bool COUNT, bool PRIMARY>
-__global__ __launch_bounds__(64, RT_WF_WAVES) void wf_trace_kernel(KParams, WfBufs) {
+// builds (WV): waves per SIMD in the low 4 bits, RT_WF_PF: each lane's next node prefetched into registers
+#define RT_WF_PF 16
+#define RT_WF_W5 5  // the default build
+template <bool COUNT, bool PRIMARY, int WV = RT_WF_W5>
+__global__ __launch_bounds__(64, WV & 15) void wf_trace_kernel(KParams, WfBufs) {
+    constexpr bool PF = (WV & RT_WF_PF) != 0;
     const void* ka = (const void*)__builtin_amdgcn_kernarg_segment_ptr();
     __shared__ int stack_lds[RT_STACK8 * RT_WAVE];
     __shared__ RefLds ref_lds;
@@ -143,6 +144,7 @@ __global__ __launch_bounds__(64, RT_WF_WAVES) void wf_trace_kernel(KParams, WfBu
     }
     Trav T;
     trav_idle(T);
+    float4 g[8];  // PF: the node the lane visits next
     Cnt cnt{};
     int src = -1;       // the query this lane traces: < n_path a path ray (camera job), else a segment
     uint32_t tag = 0u;  // a segment's shading point << 5 | light; a camera ray's output pixel
@@ -224,6 +226,7 @@ __global__ __launch_bounds__(64, RT_WF_WAVES) void wf_trace_kernel(KParams, WfBu
                                 cnt.rays++;
                                 wf_init(P.use_bvh != 0, false, S.all_opaque != 0, o, d, normalize(d), safe_inv(d),
                                         0.0f, S.ntri, T);
+                                if (PF && T.cur != RT_TRAV_NONE) node_fetch(S.nodes, T.cur, g);
                                 tracing = true;
                                 // the pixel's output row (out_row of job_pixel: setPixel's H-1-y, or band rows)
                                 tag = (uint32_t)(P.out_image ? t_row0 - (j >> 3) : t_row0 + (j >> 3)) * (uint32_t)P.W +
@@ -240,6 +243,7 @@ __global__ __launch_bounds__(64, RT_WF_WAVES) void wf_trace_kernel(KParams, WfBu
                                 wf_init(P.use_bvh != 0, seg, S.all_opaque != 0, v3{e0.x, e0.y, e0.z},
                                         v3{e1.x, e1.y, e1.z}, v3{e2.x, e2.y, e2.z}, v3{e3.x, e3.y, e3.z},
                                         seg ? e0.w : 0.0f, S.ntri, T);
+                                if (PF && T.cur != RT_TRAV_NONE) node_fetch(S.nodes, T.cur, g);
                                 tracing = true;
                             }
                         }
@@ -256,10 +260,7 @@ __global__ __launch_bounds__(64, RT_WF_WAVES) void wf_trace_kernel(KParams, WfBu
             const bool rec = leaf_pending(T);
             if (rec) trav_record<COUNT, true, false, false>(S, T, cnt, nullptr, nullptr, &ref_lds);
             const bool nv = T.cur != RT_TRAV_NONE && (!rec || (P.dual && T.lh == 0u));
-            if (nv) {
-                float4 g[8];
-                trav_node<COUNT, 8, false, true>(S, T, stk, g, cnt);
-            }
+            if (nv) trav_node<COUNT, 8, PF, true>(S, T, stk, g, cnt);
             if (!leaf_pending(T) && T.cur == RT_TRAV_NONE) {
                 trav_finish(S, T);
                 fin = true;

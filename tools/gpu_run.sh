@@ -51,7 +51,7 @@ for step in "$@"; do
            find gpurun_out/stats_${TAG}_${a:-C3} -name "*kernel_stats.csv" -exec head -3 {} \; ;;
     kstats) run 300 kstats_${TAG}_${d:-x}.log env PT_OPTS="${c//;/,}" rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/kstats_${TAG}_${d:-x} -o run -- python3 tools/prof_target.py ${a:-C3} 3 ${b:-64}
            find gpurun_out/kstats_${TAG}_${d:-x} -name "*kernel_stats.csv" -exec cat {} \; ;;
-    pmcx)  IFS=: read -r _n _a _b _c _d CTRS <<< "$step"
+    pmcx)  IFS=: read -r _n _a _b _c d CTRS <<< "$step"
            run 120 pmcx_${TAG}_${d:-x}.log env PT_OPTS="${c//;/,}" timeout -s KILL 100 rocprofv3 --pmc ${CTRS//;/ } --kernel-trace --output-format csv -d gpurun_out/pmcx_${TAG}_${d:-x} -o run -- python3 tools/prof_target.py ${a:-C3} 2 ${b:-64}
            python3 tools/pmc_by_kernel.py gpurun_out/pmcx_${TAG}_${d:-x} 2 | tee gpurun_out/pmcx_${TAG}_${d:-x}.txt | cut -c1-400 ;;
     pmc)   run 900 pmc_${TAG}_${a:-C3}.log bash tools/profile.sh ${TAG}_${a:-C3} ${a:-C3} ${b:-64} ;;
