@@ -169,6 +169,9 @@ struct rt_ctx {
     size_t wf_bytes = 0;
     int wf_trace_blocks[8] = {0};  // resident blocks of the trace kernel's builds (plain, counting)
     int opt_wf_build = 0;          // RT_OPT_WF_BUILD
+    int opt_wf_streams = 0;        // RT_OPT_WF_STREAMS (0: RT_WF_STREAMS)
+    hipStream_t wf_streams[4] = {nullptr, nullptr, nullptr, nullptr};  // the chunks' extra streams ([0] unused)
+    hipEvent_t wf_done[4] = {nullptr, nullptr, nullptr, nullptr};
 };
 
 // device ranges this library opened from other processes (rt_ipc_open): mapped for the opening device only
@@ -290,6 +293,10 @@ extern "C" int rt_destroy(rt_ctx* c) {
     if (c->d_frames) hipFree(c->d_frames);
     if (c->d_plane_tab) hipFree(c->d_plane_tab);
     if (c->d_wf) hipFree(c->d_wf);
+    for (int k = 1; k < 4; ++k) {
+        if (c->wf_streams[k]) hipStreamDestroy(c->wf_streams[k]);
+        if (c->wf_done[k]) hipEventDestroy(c->wf_done[k]);
+    }
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
     return RT_OK;
@@ -983,6 +990,10 @@ static int set_option_one(rt_ctx* c, int option, int value) {
             if (value < 0 || value > 3) break;
             c->opt_wf_build = value;
             return RT_OK;
+        case RT_OPT_WF_STREAMS:
+            if (value < 0 || value > 4) break;
+            c->opt_wf_streams = value;
+            return RT_OK;
         default:
             set_error("rt_ctx_set_option: unknown option");
             return RT_ERR_INVALID;
@@ -1378,6 +1389,8 @@ static void shape_options(const rt_ctx* c, KParams& K) {
 // ---- the wavefront path (rt_wavefront.hip) ----
 // its scope: the opaque kernel's renders with one camera sample per pixel and at most 32 lights (one bit each)
 #define RT_WF_REFILL 16             // trace kernel: waiting lanes that take new queries together (RT_OPT_WAVEFRONT 2..32)
+#define RT_WF_STREAMS 2       // streams the chunks of a large render are spread over (RT_OPT_WF_STREAMS)
+#define RT_WF_MAX_STREAMS 4
 #define RT_WF_BUDGET (64ull << 30)  // bytes of queues and shading points per chunk of camera jobs (at most; and
                                     // at most a third of the free HBM)
 static bool wf_path(const rt_ctx* c, const KParams& K) {
@@ -1387,7 +1400,6 @@ static bool wf_path(const rt_ctx* c, const KParams& K) {
 }
 
 // the trace kernel's builds (RT_OPT_WF_BUILD): 5 waves per SIMD (default), 6, 4 with the node prefetch, 8
-static const int kWfBuilds[4] = {RT_WF_W5, 6, 4 | RT_WF_PF, 8};
 template <bool COUNT, int WV>
 static int wf_occupancy(int* per_cu) {
     return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, wf_trace_kernel<COUNT, false, WV>, 64, 0);
@@ -1435,58 +1447,89 @@ static int launch_wavefront(rt_ctx* c, KParams& K, hipStream_t st, rt_stats* sta
     K.refill = c->opt_wavefront >= 2 ? c->opt_wavefront : RT_WF_REFILL;
     HIP_TRY(hipMemsetAsync(c->d_stats, 0, RT_STATS_BYTES, st));
     const int nl = std::max(1, K.S.npl + K.S.nspot);
-    // per camera job of a chunk: two hit lists (16 B), two path-ray queues (80 B), the segment queue (64 B per
-    // light) and two shading-point arrays (64 B) -- every path ray may hit
+    // the camera jobs in chunks spread over up to RT_WF_STREAMS streams, so one chunk's small levels (whose
+    // waves mostly wait on a few long queries) overlap another chunk's busy ones: per stream one set of
+    // buffers, per camera job of a chunk two hit lists (16 B), two path-ray queues (80 B), the segment queue
+    // (64 B per light) and two shading-point arrays (64 B) -- every path ray may hit
     const size_t per_job = 2 * sizeof(int4) + 2 * 80 + 64 * (size_t)nl + 2 * 64;
     size_t budget = RT_WF_BUDGET, free_b = 0, total_b = 0;
-    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) budget = std::min(budget, (size_t)(free_b / 3));
-    long long J = std::min<long long>(njobs, std::max<long long>(64, (long long)(budget / per_job)));
-    J = (J + 63) / 64 * 64;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) budget = std::min(budget, (size_t)(free_b / 3) + c->wf_bytes);
+    const int want_streams = c->opt_wf_streams > 0 ? c->opt_wf_streams : RT_WF_STREAMS;
+    const long long tiles = njobs / 64;
+    // (by default only renders of at least 1 024 tiles per stream split; an explicit RT_OPT_WF_STREAMS always does)
+    const int nstreams = (int)std::max<long long>(
+        1, std::min<long long>(want_streams, c->opt_wf_streams > 0 ? tiles : tiles / 1024));
+    long long J = std::max<long long>(64, (long long)(budget / nstreams / per_job));  // jobs per chunk (at most)
+    long long nchunks = std::max<long long>(nstreams, (njobs + J - 1) / J);
+    nchunks = (nchunks + nstreams - 1) / nstreams * nstreams;  // whole rounds of the streams
+    J = ((njobs + nchunks - 1) / nchunks + 63) / 64 * 64;
+    nchunks = (njobs + J - 1) / J;
     const size_t cnt_bytes = (sizeof(WfCnt) + 255) & ~(size_t)255;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t b_hit = al(J * sizeof(int4)), b_qp = al(J * 80), b_qs = al(J * 64 * (size_t)nl), b_nd = al(J * 64);
-    const size_t need = cnt_bytes + 2 * b_hit + 2 * b_qp + b_qs + 2 * b_nd;
-    int rc = ensure(c, &c->d_wf, &c->wf_bytes, need);
+    const size_t per_set = cnt_bytes + 2 * b_hit + 2 * b_qp + b_qs + 2 * b_nd;
+    int rc = ensure(c, &c->d_wf, &c->wf_bytes, per_set * nstreams);
     if (rc != RT_OK) return rc;
-    char* base = reinterpret_cast<char*>(c->d_wf);
-    WfBufs B{};
-    B.cnt = reinterpret_cast<WfCnt*>(base);
-    base += cnt_bytes;
-    for (int k = 0; k < 2; ++k) {
-        B.hit[k] = reinterpret_cast<int4*>(base);
-        base += b_hit;
+    WfBufs Bs[RT_WF_MAX_STREAMS];
+    for (int k = 0; k < nstreams; ++k) {
+        char* base = reinterpret_cast<char*>(c->d_wf) + per_set * k;
+        WfBufs& B = Bs[k];
+        B = WfBufs{};
+        B.cnt = reinterpret_cast<WfCnt*>(base);
+        base += cnt_bytes;
+        for (int q = 0; q < 2; ++q) {
+            B.hit[q] = reinterpret_cast<int4*>(base);
+            base += b_hit;
+        }
+        for (int q = 0; q < 2; ++q) {
+            B.qp[q] = reinterpret_cast<float4*>(base);
+            base += b_qp;
+        }
+        B.qs = reinterpret_cast<float4*>(base);
+        base += b_qs;
+        for (int q = 0; q < 2; ++q) {
+            B.nodes[q] = reinterpret_cast<float4*>(base);
+            base += b_nd;
+        }
+        B.nl = K.S.npl + K.S.nspot;
     }
-    for (int k = 0; k < 2; ++k) {
-        B.qp[k] = reinterpret_cast<float4*>(base);
-        base += b_qp;
-    }
-    B.qs = reinterpret_cast<float4*>(base);
-    base += b_qs;
-    for (int k = 0; k < 2; ++k) {
-        B.nodes[k] = reinterpret_cast<float4*>(base);
-        base += b_nd;
-    }
-    B.nl = K.S.npl + K.S.nspot;
     const int build = COUNT ? 0 : c->opt_wf_build;
     const int tgrid = wf_trace_grid(c, COUNT, build);
     int cus = 0;
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
     const int sgrid = std::max(1, cus) * 8;
+    // stream 0 is the caller's; the others start after the caller's earlier work and end before its later work
+    hipStream_t sts[RT_WF_MAX_STREAMS] = {st};
     HIP_TRY(hipEventRecord(c->ev0, st));
-    for (long long g0 = 0; g0 < njobs; g0 += J) {
+    for (int k = 1; k < nstreams; ++k) {
+        if (!c->wf_streams[k]) {
+            HIP_TRY(hipStreamCreateWithFlags(&c->wf_streams[k], hipStreamNonBlocking));
+            HIP_TRY(hipEventCreateWithFlags(&c->wf_done[k], hipEventDisableTiming));
+        }
+        sts[k] = c->wf_streams[k];
+        HIP_TRY(hipStreamWaitEvent(sts[k], c->ev0, 0));
+    }
+    for (long long ch = 0; ch < nchunks; ++ch) {
+        const int k = (int)(ch % nstreams);
+        WfBufs& B = Bs[k];
+        const long long g0 = ch * J;
         B.job0 = (int)g0;
         B.njobs = (int)std::min<long long>(J, njobs - g0);
-        HIP_TRY(hipMemsetAsync(B.cnt, 0, sizeof(WfCnt), st));
+        HIP_TRY(hipMemsetAsync(B.cnt, 0, sizeof(WfCnt), sts[k]));
         for (int l = 0; l <= K.max_level + 1; ++l) {
             B.level = l;
             if (l == 0)
-                wf_launch_trace<COUNT, true>(build, tgrid, st, K, B);
+                wf_launch_trace<COUNT, true>(build, tgrid, sts[k], K, B);
             else
-                wf_launch_trace<COUNT, false>(build, tgrid, st, K, B);
-            hipLaunchKernelGGL((wf_shade_kernel<COUNT>), dim3(sgrid), dim3(256), 0, st, K, B);
+                wf_launch_trace<COUNT, false>(build, tgrid, sts[k], K, B);
+            hipLaunchKernelGGL((wf_shade_kernel<COUNT>), dim3(sgrid), dim3(256), 0, sts[k], K, B);
         }
     }
     HIP_TRY(hipGetLastError());
+    for (int k = 1; k < nstreams; ++k) {
+        HIP_TRY(hipEventRecord(c->wf_done[k], sts[k]));
+        HIP_TRY(hipStreamWaitEvent(st, c->wf_done[k], 0));
+    }
     HIP_TRY(hipEventRecord(c->ev1, st));
     std::snprintf(c->last_kernel, sizeof(c->last_kernel), "rt::wf_trace_kernel<%s", COUNT ? "true" : "false");
     if (stats) {

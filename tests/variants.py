@@ -7,7 +7,7 @@ import contextlib
 def defaults(R):
     return {R.OPT_KERNEL: R.KERNEL_AUTO, R.OPT_VARIANT: -1, R.OPT_COOP: -1, R.OPT_COOP_MAX: 0, R.OPT_REFILL: 0,
             R.OPT_FAN: 1, R.OPT_INTERLEAVE: -1, R.OPT_FAN_CAP: 0, R.OPT_DUAL_STEP: -1, R.OPT_OPAQUE: -1,
-            R.OPT_CENTRE_FIRST: -1, R.OPT_TREE: -1, R.OPT_INTERLEAVE_TAIL: 0, R.OPT_WAVEFRONT: -1, R.OPT_WF_BUILD: 0}
+            R.OPT_CENTRE_FIRST: -1, R.OPT_TREE: -1, R.OPT_INTERLEAVE_TAIL: 0, R.OPT_WAVEFRONT: -1, R.OPT_WF_BUILD: 0, R.OPT_WF_STREAMS: 0}
 
 
 def kernel_classes(R):
@@ -49,6 +49,7 @@ def all_variants(R):
         {R.OPT_KERNEL: df, R.OPT_WAVEFRONT: 1, R.OPT_WF_BUILD: 1},  # ... its trace kernel's 6-wave build
         {R.OPT_KERNEL: df, R.OPT_WAVEFRONT: 1, R.OPT_WF_BUILD: 2},  # ... 4 waves with the node prefetch
         {R.OPT_KERNEL: df, R.OPT_WAVEFRONT: 1, R.OPT_WF_BUILD: 3},  # ... 8 waves
+        {R.OPT_KERNEL: df, R.OPT_WAVEFRONT: 1, R.OPT_WF_STREAMS: 3},  # ... its chunks over three streams
     ]
     return out
 
