@@ -1186,7 +1186,9 @@ __device__ __forceinline__ void chk_report(unsigned long long* err, uint32_t cod
 // child_base + slot), and a pop takes the group's next child at once -- front to back along the node's sort
 // axis by the ray's direction (order bit) -- where the re-visit form (node << 8) | slots re-tests the parent's
 // remaining slots first (one more node visit per pop).  Either walk gives the same lexicographic minimum.
-template <bool COUNT, int NW, bool PF = true, bool DIRECT = false, bool CHK = false>
+// LOADED (the wavefront trace kernel): the caller issued the node's loads into g before its record test, so
+// both memory round trips of a dual step overlap; nothing is prefetched
+template <bool COUNT, int NW, bool PF = true, bool DIRECT = false, bool CHK = false, bool LOADED = false>
 __device__ __forceinline__ void trav_node(const DevScene& S, Trav& T, int* stk, float4 (&g)[8], Cnt& cnt,
                                           unsigned long long* err = nullptr) {
     const uint32_t node = T.cur >> 8;
@@ -1197,7 +1199,7 @@ __device__ __forceinline__ void trav_node(const DevScene& S, Trav& T, int* stk, 
         T.lh = 0u;
         return;
     }
-    if (!PF) node_fetch(S.nodes, T.cur, g);
+    if (!PF && !LOADED) node_fetch(S.nodes, T.cur, g);
     const float4 f0 = g[0], f1 = g[1], qlx = g[2], qly = g[3], qlz = g[4], qhx = g[5], qhy = g[6], qhz = g[7];
     if (COUNT) {
         cnt.nodes++;
@@ -1309,7 +1311,7 @@ __device__ __forceinline__ void trav_node(const DevScene& S, Trav& T, int* stk, 
     } else {
         T.cur = RT_TRAV_NONE;
     }
-    if (PF && T.cur != RT_TRAV_NONE) node_fetch(S.nodes, T.cur, g);
+    if (PF && !LOADED && T.cur != RT_TRAV_NONE) node_fetch(S.nodes, T.cur, g);
 }
 
 // One postponed leaf record (the loop body of test_records).  The cursor moves to the next hit

@@ -167,7 +167,7 @@ struct rt_ctx {
     int opt_wavefront = -1;
     float* d_wf = nullptr;   // one allocation, carved by wf_layout
     size_t wf_bytes = 0;
-    int wf_trace_blocks[8] = {0};  // resident blocks of the trace kernel's builds (plain, counting)
+    int wf_trace_blocks[12] = {0};  // resident blocks of the trace kernel's builds (plain, counting)
     int opt_wf_build = 0;          // RT_OPT_WF_BUILD
     int opt_wf_streams = 0;        // RT_OPT_WF_STREAMS (0: RT_WF_STREAMS)
     hipStream_t wf_streams[4] = {nullptr, nullptr, nullptr, nullptr};  // the chunks' extra streams ([0] unused)
@@ -987,7 +987,7 @@ static int set_option_one(rt_ctx* c, int option, int value) {
             c->opt_wavefront = value;
             return RT_OK;
         case RT_OPT_WF_BUILD:
-            if (value < 0 || value > 3) break;
+            if (value < 0 || value > 5) break;
             c->opt_wf_build = value;
             return RT_OK;
         case RT_OPT_WF_STREAMS:
@@ -1405,7 +1405,7 @@ static int wf_occupancy(int* per_cu) {
     return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, wf_trace_kernel<COUNT, false, WV>, 64, 0);
 }
 static int wf_trace_grid(rt_ctx* c, bool count, int build) {
-    int& g = c->wf_trace_blocks[count ? 4 + build : build];
+    int& g = c->wf_trace_blocks[count ? 6 + build : build];
     if (g > 0) return g;
     int cus = 0, per_cu = 0;
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
@@ -1414,6 +1414,8 @@ static int wf_trace_grid(rt_ctx* c, bool count, int build) {
     else if (build == 1) e = wf_occupancy<false, 6>(&per_cu);
     else if (build == 2) e = wf_occupancy<false, 4 | RT_WF_PF>(&per_cu);
     else if (build == 3) e = wf_occupancy<false, 8>(&per_cu);
+    else if (build == 4) e = wf_occupancy<false, RT_WF_W5 | RT_WF_OVL>(&per_cu);
+    else if (build == 5) e = wf_occupancy<false, 4 | RT_WF_OVL>(&per_cu);
     else e = wf_occupancy<false, RT_WF_W5>(&per_cu);
     if (e != 0 || per_cu <= 0) per_cu = 8;
     g = std::max(1, cus) * per_cu;
@@ -1424,7 +1426,10 @@ static void wf_launch_trace(int build, int grid, hipStream_t st, const KParams& 
     if (COUNT || build == 0) hipLaunchKernelGGL((wf_trace_kernel<COUNT, PRIMARY, RT_WF_W5>), dim3(grid), dim3(64), 0, st, K, B);
     else if (build == 1) hipLaunchKernelGGL((wf_trace_kernel<false, PRIMARY, 6>), dim3(grid), dim3(64), 0, st, K, B);
     else if (build == 2) hipLaunchKernelGGL((wf_trace_kernel<false, PRIMARY, 4 | RT_WF_PF>), dim3(grid), dim3(64), 0, st, K, B);
-    else hipLaunchKernelGGL((wf_trace_kernel<false, PRIMARY, 8>), dim3(grid), dim3(64), 0, st, K, B);
+    else if (build == 3) hipLaunchKernelGGL((wf_trace_kernel<false, PRIMARY, 8>), dim3(grid), dim3(64), 0, st, K, B);
+    else if (build == 4)
+        hipLaunchKernelGGL((wf_trace_kernel<false, PRIMARY, RT_WF_W5 | RT_WF_OVL>), dim3(grid), dim3(64), 0, st, K, B);
+    else hipLaunchKernelGGL((wf_trace_kernel<false, PRIMARY, 4 | RT_WF_OVL>), dim3(grid), dim3(64), 0, st, K, B);
 }
 
 // A render as the wavefront of rt_wavefront.hip: the camera jobs in chunks whose worst-case queues fit

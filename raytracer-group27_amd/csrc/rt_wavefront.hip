@@ -114,10 +114,11 @@ __device__ __forceinline__ void wf_init(bool use_bvh, bool shadow, bool all_opaq
 #define RT_WF_BLOCK 64  // queries a wave reserves per queue-head atomic (camera jobs: one 8x8 tile)
 // builds (WV): waves per SIMD in the low 4 bits, RT_WF_PF: each lane's next node prefetched into registers
 #define RT_WF_PF 16
-#define RT_WF_W5 5  // the default build
+#define RT_WF_OVL 32  // a dual step's node loads issued before its record test (one memory round trip, not two)
+#define RT_WF_W5 5    // the default build
 template <bool COUNT, bool PRIMARY, int WV = RT_WF_W5>
 __global__ __launch_bounds__(64, WV & 15) void wf_trace_kernel(KParams, WfBufs) {
-    constexpr bool PF = (WV & RT_WF_PF) != 0;
+    constexpr bool PF = (WV & RT_WF_PF) != 0, OVL = (WV & RT_WF_OVL) != 0 && !PF;
     const void* ka = (const void*)__builtin_amdgcn_kernarg_segment_ptr();
     __shared__ int stack_lds[RT_STACK8 * RT_WAVE];
     __shared__ RefLds ref_lds;
@@ -258,9 +259,15 @@ __global__ __launch_bounds__(64, WV & 15) void wf_trace_kernel(KParams, WfBufs) 
         bool fin = false;
         if (tracing) {
             const bool rec = leaf_pending(T);
+            if (OVL) {
+                // the node this step visits, decided before the record test: the test only pops the next hit leaf
+                // (T.lh), or ends an any-hit query (then the node was loaded for nothing)
+                const uint32_t lh_after = (rec && T.rk == 0) ? (T.lh & (T.lh - 1u)) : T.lh;
+                if (T.cur != RT_TRAV_NONE && (!rec || (P.dual && lh_after == 0u))) node_fetch(S.nodes, T.cur, g);
+            }
             if (rec) trav_record<COUNT, true, false, false>(S, T, cnt, nullptr, nullptr, &ref_lds);
             const bool nv = T.cur != RT_TRAV_NONE && (!rec || (P.dual && T.lh == 0u));
-            if (nv) trav_node<COUNT, 8, PF, true>(S, T, stk, g, cnt);
+            if (nv) trav_node<COUNT, 8, PF, true, false, OVL>(S, T, stk, g, cnt);
             if (!leaf_pending(T) && T.cur == RT_TRAV_NONE) {
                 trav_finish(S, T);
                 fin = true;

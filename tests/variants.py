@@ -50,6 +50,8 @@ def all_variants(R):
         {R.OPT_KERNEL: df, R.OPT_WAVEFRONT: 1, R.OPT_WF_BUILD: 2},  # ... 4 waves with the node prefetch
         {R.OPT_KERNEL: df, R.OPT_WAVEFRONT: 1, R.OPT_WF_BUILD: 3},  # ... 8 waves
         {R.OPT_KERNEL: df, R.OPT_WAVEFRONT: 1, R.OPT_WF_STREAMS: 3},  # ... its chunks over three streams
+        {R.OPT_KERNEL: df, R.OPT_WAVEFRONT: 1, R.OPT_WF_BUILD: 4},  # ... node and record loads of a step together
+        {R.OPT_KERNEL: df, R.OPT_WAVEFRONT: 1, R.OPT_WF_BUILD: 5},  # ... the same at 4 waves
     ]
     return out
 
