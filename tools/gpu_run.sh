@@ -21,6 +21,7 @@
 #   jobs[:CFG[:OPTS]]           tools/job_trace.py (per-pixel query chains of a single frame; OPTS k=v;k=v)
 #   ranks                       bench.py N = 2 on this one GPU (gloo control plane, IPC exchange)
 #   ipc[:VIEWS]                 tools/ipc_probe.py: owner + opener of an IPC image buffer, each step timestamped
+#   ipcb:BYTES                  tools/ipc_probe.py --bytes: the IPC mapping of a buffer of BYTES alone
 #   wfcheck:CFG:VIEWS[:WxH]     tools/wf_check.py: the wavefront path against the megakernel (rays, hits, images)
 #   cpu_baseline                tools/cpu_baseline.py (BASELINE.md's full CPU samples on the host)
 #   times                       tools/time_configs.py (every config, single frame and batch)
@@ -62,6 +63,7 @@ for step in "$@"; do
     jobs)  run 300 jobs_${TAG}${b:+_$b}.log python tools/job_trace.py ${a:-C3} ${b//;/ } ;;
     ranks) run 600 ranks_${TAG}.json env BENCH_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29555 bench.py --gpus 2 --steps 5 --warmup 1 --no-single-frame ;;
     ipc)   run 150 ipc_${TAG}_v${a:-96}.log python -u tools/ipc_probe.py --views ${a:-96} --timeout 110 ;;
+    ipcb)  run 100 ipcb_${TAG}_${a}.log python -u tools/ipc_probe.py --bytes ${a} --timeout 60 ;;
     wfcheck) run 300 wfcheck_${TAG}_${a}_${b}.log python -u tools/wf_check.py ${a:-C3} ${b:-8} ${c} ;;
     cpu_baseline) run 1500 cpu_baseline_${TAG}.json python tools/cpu_baseline.py --out gpurun_out/cpu_baseline_${TAG}.out.json ;;
     times) run 900 times_${TAG}.log python tools/time_configs.py ;;
