@@ -283,13 +283,8 @@ def main():
 
     img_elems = F * W * H * 3
     exchange = "local" if (world == 1 or not bands) else args.exchange
-    if exchange == "ipc" and img_elems * 4 >= 2 ** 31:
-        # measured: two ranks storing into an IPC-mapped image buffer of 2 GiB or more (96 / 128 C3 views) stall,
-        # 64 views (1.6 GB) run; such steps take the gather scheme instead
-        if rank == 0:
-            print(f"images of {img_elems * 4 / 2 ** 30:.2f} GiB: IPC exchange limited to < 2 GiB, using --exchange gather",
-                  file=sys.stderr)
-        exchange = "gather"
+    # (images of 2 GiB or more: rt_ipc_alloc refuses them -- this ROCm's hipIpcOpenMemHandle never returns for such
+    # a buffer, tools/ipc_probe.py, DESIGN.md section 7 -- and the ranks fall back to the gather scheme below)
     ipc = None
     if exchange == "ipc":
         # rank 0's images, opened by every other rank: the ranks' kernels store their pixels into them.  Every

@@ -447,7 +447,8 @@ int rt_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[
  * rt_ipc_alloc: hipMalloc on `device` + its IPC handle (RT_IPC_HANDLE_BYTES bytes) for other processes;
  * rt_ipc_open: map another process's buffer into this one (peer access from `device`); rt_ipc_close
  * unmaps it; rt_device_free frees an rt_ipc_alloc buffer; rt_device_synchronize waits for every
- * stream of a device. */
+ * stream of a device.  rt_ipc_alloc refuses (RT_ERR_INVALID) buffers of 2 GiB or more: on this ROCm the
+ * importer's hipIpcOpenMemHandle never returns for them. */
 #define RT_IPC_HANDLE_BYTES 64
 int rt_ipc_alloc(int device, size_t bytes, void** d_ptr, uint8_t handle[RT_IPC_HANDLE_BYTES]);
 int rt_ipc_open(int device, const uint8_t handle[RT_IPC_HANDLE_BYTES], void** d_ptr);

@@ -2172,9 +2172,20 @@ extern "C" int rt_selftest_math(rt_ctx* c, const float* x, const float* y, int n
 // Rank 0 allocates the images and exports them; every rank opens them and renders its bands straight
 // into them (rt_render_views_image_device), so the framebuffer exchange is the kernels' own pixel
 // stores over xGMI while they render -- no gather step after the frame.
+// Measured on the MI355X image (ROCm 7.2, dmabuf IPC: HSA_ENABLE_IPC_MODE_LEGACY=0): hipIpcOpenMemHandle of an
+// exported buffer of 2^31 bytes or more never returns in the importing process (2 145 386 496 B maps in
+// milliseconds, 2 147 483 648 B does not return within 60 s: tools/ipc_probe.py --bytes),
+// so such a buffer is refused here, where the exporter can fall back, instead of hanging its importers.
+#define RT_IPC_MAX_BYTES ((size_t)1 << 31)
 extern "C" int rt_ipc_alloc(int device, size_t bytes, void** d_ptr, uint8_t handle[RT_IPC_HANDLE_BYTES]) {
     if (!d_ptr || !handle || bytes == 0) {
         set_error("rt_ipc_alloc: invalid argument");
+        return RT_ERR_INVALID;
+    }
+    if (bytes >= RT_IPC_MAX_BYTES) {
+        *d_ptr = nullptr;
+        set_error("rt_ipc_alloc: " + std::to_string(bytes) + " bytes: buffers of 2 GiB or more are not exported "
+                  "(this runtime's hipIpcOpenMemHandle never returns for them in the importing process)");
         return RT_ERR_INVALID;
     }
     *d_ptr = nullptr;

@@ -82,3 +82,12 @@ def test_camera_matches_oracle_bitwise(R, O):
         mine = np.array(list(cam.position) + list(cam.quat) + [cam.half_height, cam.half_width], np.float32)
         ref = O.Oracle.camera((0, 0, 0), R.default_euler(), 3.0, R.default_fovy(), R.aspect_of(W, H))
         assert mine.tobytes() == ref.tobytes()
+
+
+def test_ipc_export_of_2gib_refused(R):
+    """rt_ipc_alloc refuses buffers of 2 GiB or more before touching a device (this ROCm's importing
+    hipIpcOpenMemHandle never returns for them: 2 145 386 496 B maps, 2 147 483 648 B hangs, tools/ipc_probe.py
+    --bytes), so an exporter can fall back to the gather exchange instead of hanging its importers."""
+    for nbytes in (2 ** 31, 3 * 2 ** 30):
+        with pytest.raises(R.RtError, match="2 GiB or more"):
+            R.IpcBuffer(0, nbytes=nbytes)
