@@ -2803,7 +2803,8 @@ __device__ __forceinline__ int tree_advance(const KParams& P, TreeLane& L, int v
         int out_row;
         job_pixel(P, L.job, rpix, out_row);
         const int rows = P.out_image ? max(1, P.n_views) * P.H : (P.view_rows > 0 ? max(1, P.n_views) * P.view_rows : 0x7FFFFFFF);
-        if (out_row < 0 || out_row >= rows || (int)(rpix % (uint32_t)P.W) >= P.W) {
+        // rpix is the reference's pixel id y * W + x of one view: below W * H
+        if (out_row < 0 || out_row >= rows || rpix >= (uint32_t)P.W * (uint32_t)P.H) {
             chk_report(err, 5, (uint32_t)out_row);
             L.job = -1;
             return TA_DONE;
