@@ -1002,7 +1002,9 @@ __device__ __attribute__((noinline)) bool advance_lane_call(const void* ka, Lane
 #define RT_V_W3 8    // compiled for 3 waves per SIMD (168 VGPRs)
 #define RT_V_REVISIT 32  // opaque / tree kernels: the re-visit group stack of the other kernels (A/B), not DIRECT
 #define RT_V_CHK 64      // tree kernel: the checked build (indices validated and reported, chk_report)
-#define RT_V_WAVES(V) (((V) & RT_V_W4) ? 4 : ((V) & RT_V_W3) ? 3 : 2)
+#define RT_V_SPLIT 128   // opaque kernel: a node's shadow segment traced beside its mirror child (split_node)
+#define RT_V_W5 512      // opaque kernel: compiled for 5 waves per SIMD (96 VGPRs; with NOCOOP its LDS fits 20 blocks)
+#define RT_V_WAVES(V) (((V) & RT_V_W5) ? 5 : ((V) & RT_V_W4) ? 4 : ((V) & RT_V_W3) ? 3 : 2)
 
 
 template <bool COUNT, bool TEX, int V>
@@ -2314,17 +2316,172 @@ __device__ __forceinline__ bool lite_advance(const KParams& P, LiteLane& L, bool
     return false;
 }
 
+// ---- SPLIT: a node's shadow segment traced beside its mirror child (RT_V_SPLIT) ----
+// The lane above walks its pixel's chain one query per full-wave phase: camera ray, the node's cansee segment,
+// the mirror ray, its segment, ... -- 2 (max_level + 1) dependent phases, so a single frame ends with the waves
+// that hold the longest chains (profiles/r04/job_trace_C3_frame_interleave16.log: a job started at 5 us ends
+// with the frame).  The segment does not feed the chain: a node's colour needs its visibility, the mirror ray
+// does not.  With one light (point or spot) the lane writes each node's shading point, material and light term
+// (the light's calcColor, were it visible) to a per-lane frame in device memory, posts the segment and walks on
+// with the mirror ray; a free lane of the wave (its job done, or the owner itself once its chain has ended)
+// traces the segment and sets the node's result bits in LDS.  When the chain has ended and every segment is
+// resolved, the owner folds its nodes in level order with the same expressions as lite_advance -- colour =
+// 0 + term if visible, acc = acc + w * colour, w = lite_child_weight -- and stores the sample, so the values,
+// their order and the ray count are unchanged.  Between phases the lane keeps 3 dwords instead of LiteLane's 24.
+struct SplitLane {
+    int job;                 // >= 0 job; -1 idle (fetch another or take a segment); -2 no more work
+    uint32_t sample : 7;     // camera sample
+    uint32_t level : 5;      // level of the node the lane's own query looks for
+    uint32_t cdone : 1;      // the sample's mirror chain has ended (segments may be outstanding)
+    uint32_t tk : 1;         // the query in flight is the segment of lane tk_owner's node tk_level
+    uint32_t tk_owner : 6;
+    uint32_t tk_level : 4;
+    uint32_t nlev : 5;       // nodes of the sample in the frame: levels 0 .. nlev - 1
+    uint32_t untaken : 16;   // levels whose segment is posted and not taken
+    uint32_t posted : 16;    // levels with a segment
+};
+
+// frame of lane `lane`'s node `level`: (shading point, material), (colour, or the light term of a posted segment)
+__device__ __forceinline__ float4* split_frame(const KParams& P, int lane, int level) {
+    return P.frames + ((size_t)level * P.frame_slots + blockIdx.x * RT_WAVE + lane) * 2;
+}
+
+// the scene's one light (src/shadow.cpp: point lights first, then spot lights)
+__device__ __forceinline__ void split_light(const DevScene& S, v3& lp, v3& lc) {
+    if (S.npl > 0) {
+        const rt_point_light pl = S.pl[0];
+        lp = ld3(pl.position);
+        lc = ld3(pl.color);
+    } else {
+        const DSpot sp = S.spot[0];
+        lp = ld3(sp.pos);
+        lc = ld3(sp.color);
+    }
+}
+
+// start_cansee toward the light (lite_next_light): false if the light lies within SHADOW_ERROR_OFFSET
+__device__ __forceinline__ bool split_segment(v3 hp, v3 lp, Query& q, float& sdist) {
+    v3 d = lp - hp;
+    sdist = length(d);
+    d = normalize(d);
+    if (!(sdist > 0.0005f)) return false;
+    q.o = hp + 0.0005f * d;
+    q.d = d;
+    q.t = FLT_MAX;
+    return true;
+}
+
+// the i-th (0-based) set bit of m (i < popcount(m))
+__device__ __forceinline__ int nth_set(uint64_t m, int i) {
+    int pos = 0;
+#pragma unroll
+    for (int w = 32; w >= 1; w >>= 1) {
+        const int c = __popcll(m & ((1ull << w) - 1ull));
+        if (i >= c) {
+            i -= c;
+            m >>= w;
+            pos += w;
+        }
+    }
+    return pos;
+}
+
+// The lane's own query (camera or mirror ray) finished: its node into the frame, its segment posted, and true
+// with the mirror ray in q; false when the chain ends (a miss, the last level, or no specular colour).
+template <bool COUNT>
+__device__ __forceinline__ bool split_node(const KParams& P, SplitLane& L, int lane, bool hit, const Best& b, Query& q,
+                                           Cnt& cnt) {
+    const DevScene& S = P.S;
+    if (!hit) {
+        L.cdone = 1;
+        return false;
+    }
+    const Surf s = surface(S, q.o, q.d, b, false, L.level == 0);
+    if (COUNT) {
+        cnt.hits++;
+        if (s.ub) cnt.ub++;
+    }
+    const v3 hp = s.p, nN = normalize(s.n), refl = reflect(normalize(q.d), nN);
+    const int mat = (b.rec >= 0) ? s.mesh : b.rec;
+    v3 lp, lc, color{0.0f, 0.0f, 0.0f};
+    split_light(S, lp, lc);
+    bool post = false;
+    const bool lit = (S.npl > 0) || dot(normalize(ld3(S.spot[0].dir)), normalize(hp - lp)) > S.spot[0].cos_angle;
+    if (lit) {
+        Query sq;
+        float sd;
+        post = split_segment(hp, lp, sq, sd);
+        const v3 ldir = normalize(lp - hp);  // lite_light_visible
+        const float cosL = fabsf(dot(nN, ldir));
+        const float d2 = dot(normalize(refl), ldir);
+        const v3 t = calc_color(lc, 1.0f, cosL, (0.0f < d2) ? d2 : 0.0f, load_mat(S, mat));
+        if (post) color = t;   // folded as 0 + t once the segment finds the light visible
+        else color += t;       // visible without a query
+    }
+    float4* f = split_frame(P, lane, L.level);
+    f[0] = make_float4(hp.x, hp.y, hp.z, __int_as_float(mat));
+    f[1] = make_float4(color.x, color.y, color.z, 0.0f);
+    if (post) {
+        L.untaken |= 1u << L.level;
+        L.posted |= 1u << L.level;
+    }
+    L.nlev = L.level + 1;
+    if (L.level < P.max_level) {
+        const v3 ks{s.m.ks[0], s.m.ks[1], s.m.ks[2]};
+        if (ks.x > 0.0f || ks.y > 0.0f || ks.z > 0.0f) {
+            L.level++;
+            q.o = hp + 0.01f * refl;
+            q.d = refl;
+            q.t = FLT_MAX;
+            return true;
+        }
+    }
+    L.cdone = 1;
+    return false;
+}
+
+// the posted segment of lane `owner`'s node `level`, rebuilt from its shading point
+__device__ __forceinline__ void split_take(const KParams& P, int owner, int level, Query& q, float& sdist) {
+    const float4 a = split_frame(P, owner, level)[0];
+    v3 lp, lc;
+    split_light(P.S, lp, lc);
+    split_segment(v3{a.x, a.y, a.z}, lp, q, sdist);
+}
+
+// the sample's colour: its nodes in level order (lite_advance's fold; res: LDS result bits, done | visible << 16)
+__device__ __forceinline__ v3 split_fold(const KParams& P, const SplitLane& L, int lane, uint32_t res) {
+    v3 acc{0.0f, 0.0f, 0.0f}, w{1.0f, 1.0f, 1.0f};
+    for (int l = 0; l < (int)L.nlev; ++l) {
+        const float4* f = split_frame(P, lane, l);
+        const float4 a = f[0], c = f[1];
+        v3 color{c.x, c.y, c.z};
+        if ((L.posted >> l) & 1u) {
+            const v3 zero{0.0f, 0.0f, 0.0f};
+            color = ((res >> (16 + l)) & 1u) ? zero + color : zero;
+        }
+        acc = acc + w * color;
+        if (l + 1 < (int)L.nlev) {  // lite_child_weight of node l
+            const DMat m = load_mat(P.S, __float_as_int(a.w));
+            const v3 ks{m.ks[0], m.ks[1], m.ks[2]};
+            w = (m.shin != 0.0f) ? w * ((ks * ks) / (float)P.glossy_n) : w * (ks * ks);
+        }
+    }
+    return acc;
+}
+
 template <bool COUNT, int V>
 __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KParams, JobSrc) {
     constexpr bool PF = !(V & RT_V_NOPF), COOP = !(V & RT_V_NOCOOP), DIRECT = !(V & RT_V_REVISIT);
+    constexpr bool SPLIT = (V & RT_V_SPLIT) != 0;
     // the kernel's arguments are read where each phase uses them (fresh_kernarg), not held in SGPRs
     const void* ka = (const void*)__builtin_amdgcn_kernarg_segment_ptr();
 #define RT_FRESH const KParams& P = *(const KParams*)fresh_kernarg(ka); const DevScene& S = P.S
     __shared__ int stack_lds[RT_STACK8 * RT_WAVE];
-    __shared__ int coop_pool[COOP_POOL];   // drain lane groups (COOP): node groups of the wave's last queries
-    __shared__ int coop_q[CQ_N * COOP_Q];  // ... and those queries
+    __shared__ int coop_pool[COOP ? COOP_POOL : 1];   // drain lane groups (COOP): node groups of the wave's last queries
+    __shared__ int coop_q[COOP ? CQ_N * COOP_Q : 1];  // ... and those queries
     __shared__ int s_base, s_lim;
     __shared__ RefLds ref_lds;             // the reference BVH's boxes and leaf paths (candidate culling)
+    __shared__ uint32_t split_res[SPLIT ? RT_WAVE : 1];  // SPLIT: per owner lane, segments done | visible << 16
     const int lane_id = threadIdx.x;
     int* stk = stack_lds + lane_id;
     if (RT_REF_LDS) {
@@ -2333,9 +2490,15 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
     }
     const unsigned long long t_wave0 = (COUNT && kernel_params(ka).wave_trace) ? wall_clock64() : 0ull;
     unsigned int wave_jobs = 0;
-    LiteLane L;
+    std::conditional_t<SPLIT, SplitLane, LiteLane> L;
     L.job = -1;
-    L.shadow = false;
+    if constexpr (SPLIT) {
+        L.tk = 0;
+        L.cdone = 0;
+        L.untaken = L.posted = 0;
+    } else {
+        L.shadow = false;
+    }
     Trav T;
     Cnt cnt{};
     SlabCnt slab{};
@@ -2349,16 +2512,92 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
         RT_FRESH;
         const JobSrc& J = kernel_jobs(&P);
         if (COUNT && P.wave_trace && t_exh) pa_drain++;
-        bool start = false;
+        bool start = false, qshadow = false;
         Query q;
         float qsdist = 0.0f;
-        if (pending) {
+        if constexpr (SPLIT) {
+            if (COUNT) {
+                const bool ap = __any(pending);
+                if (ap && wave_leader()) cnt.wadv++;
+            }
+            // a taken segment finished: its visibility to the owner (visible iff no candidate)
+            if (pending && L.tk) {
+                pending = false;
+                atomicOr(&split_res[L.tk_owner], (1u << L.tk_level) | (T.found ? 0u : (1u << (16 + L.tk_level))));
+                L.tk = 0;
+            }
+            __syncthreads();
+            // the lane's own camera / mirror query finished: its node into the frame, the mirror ray next
+            if (pending) {
+                pending = false;
+                q.o = T.o;
+                q.d = T.d;
+                start = split_node<COUNT>(P, L, lane_id, T.found, T.best, q, cnt);
+            }
+            // the chain has ended: its own untaken segments first, then the fold once every segment is resolved
+            if (L.job >= 0 && L.cdone && !start) {
+                if (L.untaken) {
+                    const int lv = __ffs(L.untaken) - 1;
+                    L.untaken &= L.untaken - 1u;
+                    split_take(P, lane_id, lv, q, qsdist);
+                    L.tk = 1;
+                    L.tk_owner = lane_id;
+                    L.tk_level = lv;
+                    start = qshadow = true;
+                } else {
+                    const uint32_t r = split_res[lane_id];
+                    if ((r & 0xFFFFu) == L.posted) {
+                        const v3 acc = split_fold(P, L, lane_id, r);
+                        const int jb = L.job;
+                        if (store_sample(P, L.job, L.sample, acc)) {
+                            L.sample++;
+                            uint32_t rpix;
+                            int out_row;
+                            job_pixel(P, L.job, rpix, out_row);
+                            camera_query(P, L.job, rpix, L.sample, q);
+                            L.level = 0;
+                            L.cdone = 0;
+                            L.nlev = 0;
+                            L.untaken = L.posted = 0;
+                            split_res[lane_id] = 0u;
+                            start = true;
+                        } else {
+                            L.job = -1;
+                            if (COUNT && P.job_trace) P.job_trace[3 * jb + 1] = wall_clock64();
+                        }
+                    }
+                }
+            }
+            // free lanes take posted segments: the oldest of each owner, owners in lane order
+            {
+                const bool fr = L.job < 0 && !start;
+                const uint32_t ut = L.untaken;
+                const unsigned long long om = __ballot(ut != 0u), fm = __ballot(fr);
+                if (om && fm) {
+                    const int n = min(__popcll(om), __popcll(fm));
+                    const int rf = __popcll(fm & ((1ull << lane_id) - 1ull));
+                    const int ro = __popcll(om & ((1ull << lane_id) - 1ull));
+                    const int owner = nth_set(om, (fr && rf < n) ? rf : 0);
+                    const uint32_t out = (uint32_t)__shfl((int)ut, owner);
+                    if (fr && rf < n) {
+                        const int lv = __ffs(out) - 1;
+                        split_take(P, owner, lv, q, qsdist);
+                        L.tk = 1;
+                        L.tk_owner = owner;
+                        L.tk_level = lv;
+                        start = qshadow = true;
+                    }
+                    if (ut && ro < n) L.untaken = ut & (ut - 1u);
+                }
+            }
+        } else if (pending) {
             pending = false;
             if (COUNT && wave_leader()) cnt.wadv++;
             q.o = T.o;
             q.d = T.d;
             const int jb = L.job;
             start = lite_advance<COUNT>(P, L, T.found, T.best, q, qsdist, cnt);
+            qshadow = L.shadow;
             if (COUNT && P.job_trace && L.job == -1) P.job_trace[3 * jb + 1] = wall_clock64();
         }
         const unsigned long long tJ = COUNT ? (unsigned long long)clock64() : 0ull;
@@ -2390,11 +2629,19 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
                     if (job_pixel(P, job_k, rpix, out_row)) {
                         L.sample = 0;
                         camera_query(P, job_k, rpix, 0, q);
-                        L.acc = v3{0.0f, 0.0f, 0.0f};
-                        L.w = v3{1.0f, 1.0f, 1.0f};
                         L.level = 0;
-                        L.desc = false;
-                        L.shadow = false;
+                        if constexpr (SPLIT) {
+                            L.cdone = 0;
+                            L.nlev = 0;
+                            L.untaken = L.posted = 0;
+                            split_res[lane_id] = 0u;
+                        } else {
+                            L.acc = v3{0.0f, 0.0f, 0.0f};
+                            L.w = v3{1.0f, 1.0f, 1.0f};
+                            L.desc = false;
+                            L.shadow = false;
+                        }
+                        qshadow = false;
                         qsdist = 0.0f;
                         start = true;
                     } else {
@@ -2415,7 +2662,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
             Trav Tn;
             if (start) {
                 cnt.rays++;
-                trav_init_q(S, P.use_bvh != 0, q.o, q.d, q.t, L.shadow, qsdist, Tn);
+                trav_init_q(S, P.use_bvh != 0, q.o, q.d, q.t, qshadow, qsdist, Tn);
                 tracing = true;
             } else {
                 trav_idle(Tn);
@@ -2424,7 +2671,8 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
         }
         if (COUNT && P.wave_trace && !t_exh && __any(L.job == -2)) t_exh = wall_clock64();
         if (!__any(tracing)) {
-            if (!__any(L.job == -1 || pending)) break;  // every lane exhausted
+            // every lane exhausted (SPLIT: an owner waits only on a segment some lane is tracing)
+            if (!__any(L.job == -1 || pending || (SPLIT && L.job >= 0))) break;
             continue;
         }
         // ---- phase B: one node visit and / or one leaf record per lane and iteration ----

@@ -105,7 +105,7 @@ struct rt_ctx {
     bool df_ok = true;  // the BVH8 fits the dynamic-fetch kernel's LDS stack
     bool glossy_material = false;  // opaque, ks > 0, shininess != 0 (glossy_ray_count > 1 draws lobes)
     int persistent_blocks[1024] = {0};  // resident 64-lane blocks per (kernel class, variant)
-    int opaque_blocks[2] = {0, 0};      // ... of the opaque-scene kernel (4 / 3 waves per SIMD)
+    int opaque_blocks[6] = {0, 0, 0, 0, 0, 0};  // ... of the opaque-scene kernel (4 / 3 waves per SIMD; SPLIT; A/Bs)
     int tree_blocks[3] = {0, 0, 0};     // ... of the recursion-tree kernel (3-wave, re-visit, checked 4-wave)
     // recursion-tree kernel: the lanes' pending refracted rays (KParams::frames)
     float* d_frames = nullptr;
@@ -967,7 +967,7 @@ static int set_option_one(rt_ctx* c, int option, int value) {
             c->opt_variant = value;
             return RT_OK;
         case RT_OPT_OPAQUE:
-            if (value < -1 || value > 3) break;
+            if (value < -1 || value > 7) break;
             c->opt_opaque = value;
             return RT_OK;
         case RT_OPT_TREE:
@@ -1060,14 +1060,24 @@ static bool opaque_path(const rt_ctx* c, const KParams& K, bool pixels) {
     return pixels && c->opt_opaque != 0 && c->opt_variant < 0 && use_df(c, K) && K.S.all_opaque && K.S.nsl == 0 &&
            K.S.nplane == 0 && !K.S.tex_on && (K.glossy_n == 1 || !c->glossy_material);
 }
-// the opaque kernel's build: the 4-wave one for batches and single frames (round 4, with the direct group stack
-// and the leaf bound 2: C3 frame 1.237 vs 1.246 ms at 3 waves, profiles/r04/ab_r04g_refill.log; the 3-wave build
-// had won frames before); RT_OPT_OPAQUE 2 the 3-wave build, 3 the 4-wave re-visit A/B
+// the opaque kernel's build: 4 waves per SIMD for batches and single frames (round 4, with the direct group stack
+// and the leaf bound 2: C3 frame 1.237 vs 1.246 ms at 3 waves, profiles/r04/ab_r04g_refill.log), with SPLIT (a
+// node's shadow segment traced beside its mirror child, rt_megakernel.hip split_node) where the scene has one
+// light (point or spot) and at most 16 levels (the LDS result bits): its lane keeps 3 dwords between phases, so
+// the 4-wave build has no spills (31 VGPRs before) -- C3 64-view batch 0.376-0.378 -> 0.373 ms/frame, frame
+// 1.045-1.074 -> 0.95-0.97 ms (profiles/r05/ab_r05m.log, ab_r05n.log).  RT_OPT_OPAQUE 1 the 4-wave build without
+// SPLIT, 2 the 3-wave build, 3 the 4-wave re-visit A/B, 4 / 5 SPLIT at 4 / 3 waves, 6 / 7 SPLIT without the
+// drain lane groups at 5 / 4 waves (A/Bs: 0.388 / 0.377 ms/frame, frames 1.26 / 1.14 ms)
+#define RT_OPAQUE_V5S (RT_V_W5 | RT_V_NOPF | RT_V_NOCOOP | RT_V_SPLIT)   // A/B: 5 waves, no drain lane groups
+#define RT_OPAQUE_V4SN (RT_V_W4 | RT_V_NOPF | RT_V_NOCOOP | RT_V_SPLIT)  // A/B: 4 waves, no drain lane groups
+static bool split_ok(const KParams& K) { return K.S.npl + K.S.nspot == 1 && K.max_level < 16; }
 static int opaque_variant(const rt_ctx* c, const KParams& K) {
-    (void)K;
     if (c->opt_opaque == 2) return RT_OPAQUE_V3;
     if (c->opt_opaque == 3) return RT_OPAQUE_V | RT_V_REVISIT;
-    return RT_OPAQUE_V;
+    if (c->opt_opaque == 1 || !split_ok(K)) return RT_OPAQUE_V;
+    if (c->opt_opaque == 6) return RT_OPAQUE_V5S;
+    if (c->opt_opaque == 7) return RT_OPAQUE_V4SN;
+    return (c->opt_opaque == 5 ? RT_OPAQUE_V3 : RT_OPAQUE_V) | RT_V_SPLIT;
 }
 
 // the recursion-tree kernel (rt_megakernel.hip persistent_tree_kernel): 4 / 3 waves per SIMD
@@ -1129,6 +1139,14 @@ static int launch_persistent(int grid, hipStream_t st, const KParams& K, const J
                                K, J);
         } else if (v == RT_OPAQUE_V3) {
             hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V3>), dim3(grid), dim3(64), 0, st, K, J);
+        } else if (v == (RT_OPAQUE_V | RT_V_SPLIT)) {
+            hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V | RT_V_SPLIT>), dim3(grid), dim3(64), 0, st, K, J);
+        } else if (v == (RT_OPAQUE_V3 | RT_V_SPLIT)) {
+            hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V3 | RT_V_SPLIT>), dim3(grid), dim3(64), 0, st, K, J);
+        } else if (v == RT_OPAQUE_V5S) {
+            hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V5S>), dim3(grid), dim3(64), 0, st, K, J);
+        } else if (v == RT_OPAQUE_V4SN) {
+            hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V4SN>), dim3(grid), dim3(64), 0, st, K, J);
         } else {
             hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V>), dim3(grid), dim3(64), 0, st, K, J);
         }
@@ -1177,13 +1195,17 @@ static int occupancy_of(int* per_cu) {
 static int persistent_grid(rt_ctx* c, const KParams& K, bool pixels) {
     if (opaque_path(c, K, pixels)) {
         const int v = opaque_variant(c, K);
-        const int key = (v & RT_V_W3) ? 1 : 0;  // 3 or 4 waves per SIMD
+        const int key = v == RT_OPAQUE_V5S ? 4 : v == RT_OPAQUE_V4SN ? 5 : ((v & RT_V_W3) ? 1 : 0) + ((v & RT_V_SPLIT) ? 2 : 0);
         if (c->opaque_blocks[key] > 0) return c->opaque_blocks[key];
         int cus = 0, per_cu = 0;
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
         const hipError_t e =
-            key ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V3>, 64, 0)
-                : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V>, 64, 0);
+            key == 5   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V4SN>, 64, 0)
+            : key == 4 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V5S>, 64, 0)
+            : key == 3 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V3 | RT_V_SPLIT>, 64, 0)
+            : key == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V | RT_V_SPLIT>, 64, 0)
+            : key == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V3>, 64, 0)
+                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V>, 64, 0);
         if (e != hipSuccess || per_cu <= 0) per_cu = 8;
         c->opaque_blocks[key] = std::max(1, cus) * per_cu;
         return c->opaque_blocks[key];
@@ -1579,6 +1601,13 @@ static int launch_render(rt_ctx* c, KParams& K, hipStream_t st, int count_mode, 
             // the tree kernel's frame stacks: max_level frames of 48 B per resident lane
             const size_t slots = (size_t)grid * 64;
             const int rc = ensure(c, &c->d_frames, &c->frames_bytes, slots * std::max(1, K.max_level) * 48);
+            if (rc != RT_OK) return rc;
+            K.frames = reinterpret_cast<float4*>(c->d_frames);
+            K.frame_slots = (int)slots;
+        } else if (opaque_path(c, K, true) && (opaque_variant(c, K) & RT_V_SPLIT)) {
+            // SPLIT: max_level + 1 node frames of 32 B per resident lane
+            const size_t slots = (size_t)grid * 64;
+            const int rc = ensure(c, &c->d_frames, &c->frames_bytes, slots * (K.max_level + 1) * 32);
             if (rc != RT_OK) return rc;
             K.frames = reinterpret_cast<float4*>(c->d_frames);
             K.frame_slots = (int)slots;

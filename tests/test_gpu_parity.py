@@ -284,6 +284,7 @@ def test_kernel_variants_bit_identical(R, ctxs, golden_dir, case):
 @pytest.mark.parametrize("cfg,uv,kernel,aa", [("C2", None, "", 0), ("C2", None, "df", 0), ("C2", None, "df", 1),
                                               ("C3", (200, 80), "", 0), ("C3", (200, 80), "tail", 0),
                                               ("C3", (200, 80), "wf", 0), ("C2", None, "wf", 0),
+                                              ("C3", (200, 80), "split", 0), ("C3", (200, 80), "split", 1),
                                               ("C4", (200, 80), "", 0), ("C5", None, "", 0)])
 def test_view_batch_bit_identical(R, O, ctxs, cfg, uv, kernel, aa):
     """rt_render_views_device: every view of a batch is bit-identical to rt_render_device with that
@@ -297,6 +298,8 @@ def test_view_batch_bit_identical(R, O, ctxs, cfg, uv, kernel, aa):
         opts = {R.OPT_KERNEL: R.KERNEL_DYNAMIC_FETCH, R.OPT_INTERLEAVE_TAIL: 2}
     if kernel == "wf":  # the wavefront path (trace / shade kernels per recursion level)
         opts = {R.OPT_KERNEL: R.KERNEL_DYNAMIC_FETCH, R.OPT_WAVEFRONT: 1}
+    if kernel == "split":  # the opaque kernel with the shadow segments traced beside the mirror chain
+        opts = {R.OPT_KERNEL: R.KERNEL_DYNAMIC_FETCH, R.OPT_OPAQUE: 4}
     with V.options(R, ctx, opts):
         _view_batch_checks(R, O, scene, ctx, prm, cfg, aa)
 

@@ -34,9 +34,12 @@ def all_variants(R):
         {R.OPT_KERNEL: df, R.OPT_VARIANT: R.DF_BATCH, R.OPT_DUAL_STEP: 0},
         {R.OPT_KERNEL: df, R.OPT_VARIANT: R.DF_ALT, R.OPT_COOP: 2, R.OPT_REFILL: 64},  # out-of-line drain, steady state
         {R.OPT_KERNEL: df, R.OPT_OPAQUE: 0},                    # general kernels where the opaque one is eligible
-        {R.OPT_KERNEL: df, R.OPT_OPAQUE: 1},                    # the opaque kernel's 4-wave (batch) build
+        {R.OPT_KERNEL: df, R.OPT_OPAQUE: 1},                    # the opaque kernel's 4-wave build without SPLIT
         {R.OPT_KERNEL: df, R.OPT_OPAQUE: 2},                    # ... its 3-wave build
         {R.OPT_KERNEL: df, R.OPT_OPAQUE: 3},                    # ... its 4-wave build with the re-visit group stack
+        {R.OPT_KERNEL: df, R.OPT_OPAQUE: 4},                    # ... its 4-wave build, segments beside the mirror chain
+        {R.OPT_KERNEL: df, R.OPT_OPAQUE: 5},                    # ... the same in the 3-wave build
+        {R.OPT_KERNEL: df, R.OPT_OPAQUE: 7},                    # ... SPLIT without the drain lane groups
         {R.OPT_KERNEL: df, R.OPT_REFILL: 32},                   # ... and a half-wave refill
         {R.OPT_KERNEL: df, R.OPT_COOP: 1},                      # ... drain lane groups in the drain only
         {R.OPT_KERNEL: df, R.OPT_TREE: 0},                      # general kernels where the tree kernel is eligible
