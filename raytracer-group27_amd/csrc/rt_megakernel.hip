@@ -2506,6 +2506,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
     bool tracing = false, pending = false;
     unsigned long long t_exh = 0ull;
     unsigned int it_drain = 0, lanes_drain = 0, coop_n = 0, pa_drain = 0;  // wave trace, counting builds only
+    uint32_t qn0 = 0, qr0 = 0;  // counting builds: the lane's node / record counts when its query started
     for (;;) {
         // ---- phase A: advance the pending lanes, then refill the idle ones ----
         unsigned long long tA = COUNT ? (unsigned long long)clock64() : 0ull;
@@ -2664,6 +2665,12 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
                 cnt.rays++;
                 trav_init_q(S, P.use_bvh != 0, q.o, q.d, q.t, qshadow, qsdist, Tn);
                 tracing = true;
+                // counting builds: queries whose direction is not unit walk every record (debug counter 28)
+                if (COUNT && Tn.cur == RT_TRAV_NONE && Tn.rk > 0) atomicAdd(P.stats + RT_STATS_EXTRA + 12, 1ull);
+                if (COUNT) {
+                    qn0 = cnt.nodes;
+                    qr0 = cnt.tris;
+                }
             } else {
                 trav_idle(Tn);
             }
@@ -2710,6 +2717,13 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
                 trav_finish(S, T);
                 tracing = false;
                 pending = true;
+                // counting builds: the longest queries (debug counters 29 / 30: most node visits / records of one
+                // query, 31: queries with more than 512 node visits)
+                if (COUNT) {
+                    atomicMax(P.stats + RT_STATS_EXTRA + 13, (unsigned long long)(cnt.nodes - qn0));
+                    atomicMax(P.stats + RT_STATS_EXTRA + 14, (unsigned long long)(cnt.tris - qr0));
+                    if (cnt.nodes - qn0 > 512u) atomicAdd(P.stats + RT_STATS_EXTRA + 15, 1ull);
+                }
             }
             // full-wave phases (refill 64, the batch and few-sample policy of the general kernel): the phase
             // ends when no lane traces
