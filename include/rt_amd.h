@@ -383,7 +383,7 @@ int rt_debug_counters(rt_ctx* ctx, uint64_t* out, int n);
 #define RT_OPT_COOP 2        /* drain lane groups: -1 by render shape, 0 off, 1 drain only, 2 + full-wave stragglers */
 #define RT_OPT_COOP_MAX 3    /* most queries handed to lane groups (0: as many as the LDS pool allows) */
 #define RT_OPT_REFILL 4      /* dynamic-fetch kernel: waiting lanes that end a traversal phase (0: by shape) */
-#define RT_OPT_WAVE_TRACE 5  /* 1: record rt_debug_wave_trace data */
+#define RT_OPT_WAVE_TRACE 5  /* 1: record rt_debug_wave_trace data; 2: also rt_debug_phase_trace */
 #define RT_OPT_VARIANT 6     /* developer A/B: compiled kernel variant (rt_megakernel.hip RT_V_*), -1 default */
 #define RT_OPT_FAN_CAP 9     /* fan renders: pixels a wave may have waiting on fans before it takes no new ones (0: default 16) */
 #define RT_OPT_INTERLEAVE 8  /* job -> pixel order: -1 by render shape, 0 8x8 tiles per wave, 1 one pixel of each of 64 tiles per wave, k = 2..5 64 / 2^k pixels of each of 2^k tiles */
@@ -409,6 +409,12 @@ int rt_debug_wave_trace(rt_ctx* ctx, uint64_t* out, int max_waves);
 /* ... and per job (pixel) of that launch: 3 words (start, end, queries of the job); out holds
  * 3 * max_jobs words.  Returns the job count. */
 int rt_debug_job_trace(rt_ctx* ctx, uint64_t* out, int max_jobs);
+/* ... and with RT_OPT_WAVE_TRACE = 2 (the opaque kernel's counting build), the wave's first RT_PHASE_EV traversal
+ * phases: 2 words each (start | tracing lanes << 48, end | traversal iterations << 40 | lane groups << 63; start
+ * and end relative to the wave's start, rt_debug_wave_trace word 0);
+ * out holds 2 * RT_PHASE_EV * max_waves words.  Returns the wave count. */
+#define RT_PHASE_EV 512
+int rt_debug_phase_trace(rt_ctx* ctx, uint64_t* out, int max_waves);
 /* rt_create's phase clock, cumulative ms (device, reference BVH, BVH2/BVH8, records, materials and
  * textures, uploads, total): up to n doubles. */
 int rt_debug_create_ms(rt_ctx* ctx, double* out, int n);

@@ -111,6 +111,7 @@ struct KParams {
     uint32_t seed_lo, seed_hi;  // glossy sampling: Philox-4x32-10 key (rt_params.rng_seed)
     unsigned long long* wave_trace;  // developer wave trace (rt_ctx_set_option RT_OPT_WAVE_TRACE), or null
     unsigned long long* job_trace;   // ... and per job: start, end (100 MHz clock), queries
+    unsigned long long* phase_trace; // ... and per wave RT_PHASE_EV traversal phases (RT_OPT_WAVE_TRACE 2), or null
     int coop;                        // dynamic-fetch kernel: lane-group traversal of the drain's queries
     int coop_max;                    // ... when at most this many queries are left in the wave
     int coop_reserve;                // ... free pool slots kept for depth-first steps

@@ -2507,6 +2507,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
     unsigned long long t_exh = 0ull;
     unsigned int it_drain = 0, lanes_drain = 0, coop_n = 0, pa_drain = 0;  // wave trace, counting builds only
     uint32_t qn0 = 0, qr0 = 0;  // counting builds: the lane's node / record counts when its query started
+    uint32_t nph = 0;           // counting builds with a phase trace: the wave's traversal phases so far
     for (;;) {
         // ---- phase A: advance the pending lanes, then refill the idle ones ----
         unsigned long long tA = COUNT ? (unsigned long long)clock64() : 0ull;
@@ -2666,7 +2667,9 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
                 trav_init_q(S, P.use_bvh != 0, q.o, q.d, q.t, qshadow, qsdist, Tn);
                 tracing = true;
                 // counting builds: queries whose direction is not unit walk every record (debug counter 28)
-                if (COUNT && Tn.cur == RT_TRAV_NONE && Tn.rk > 0) atomicAdd(P.stats + RT_STATS_EXTRA + 12, 1ull);
+                // (wave trace 1 only: these per-query atomics on one word would distort the other traces' clocks)
+                if (COUNT && P.wave_trace && !P.phase_trace && Tn.cur == RT_TRAV_NONE && Tn.rk > 0)
+                    atomicAdd(P.stats + RT_STATS_EXTRA + 12, 1ull);
                 if (COUNT) {
                     qn0 = cnt.nodes;
                     qr0 = cnt.tris;
@@ -2691,7 +2694,14 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
         float4 g[8];
         if (PF && tracing && T.cur != RT_TRAV_NONE) node_fetch(S.nodes, T.cur, g);
         bool to_coop = false;  // the loop ended for the lane groups (not for a partial refill)
+        unsigned long long t_ph = 0ull;
+        uint32_t ntr_ph = 0, it_ph = 0;
+        if (COUNT && P.phase_trace) {
+            t_ph = wall_clock64();
+            ntr_ph = (uint32_t)__popcll(__ballot(tracing));
+        }
         for (;;) {
+            if (COUNT && P.phase_trace) ++it_ph;
             if (COUNT) {
                 const int ntr = __popcll(__ballot(tracing));
                 if (wave_leader()) cnt.hist[min((ntr - 1) >> 4, 2)]++;
@@ -2719,7 +2729,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
                 pending = true;
                 // counting builds: the longest queries (debug counters 29 / 30: most node visits / records of one
                 // query, 31: queries with more than 512 node visits)
-                if (COUNT) {
+                if (COUNT && P.wave_trace && !P.phase_trace) {
                     atomicMax(P.stats + RT_STATS_EXTRA + 13, (unsigned long long)(cnt.nodes - qn0));
                     atomicMax(P.stats + RT_STATS_EXTRA + 14, (unsigned long long)(cnt.tris - qr0));
                     if (cnt.nodes - qn0 > 512u) atomicAdd(P.stats + RT_STATS_EXTRA + 15, 1ull);
@@ -2788,6 +2798,16 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
                 pending = true;
             }
             if (COUNT && P.wave_trace) coop_n++;
+        }
+        if (COUNT && P.phase_trace) {
+            if (lane_id == 0 && nph < RT_PHASE_EV) {
+                unsigned long long* w = P.phase_trace + ((size_t)blockIdx.x * RT_PHASE_EV + nph) * 2;
+                // times relative to the wave's start (wave trace word 0), in 40 bits
+                w[0] = (t_ph - t_wave0) | ((unsigned long long)ntr_ph << 48);
+                w[1] = (wall_clock64() - t_wave0) | ((unsigned long long)it_ph << 40) |
+                       ((unsigned long long)(to_coop ? 1 : 0) << 63);
+            }
+            ++nph;
         }
         if (COUNT) cnt.cyc_b += (unsigned long long)clock64() - tB;
     }

@@ -117,6 +117,7 @@ struct rt_ctx {
     float* d_wave_trace = nullptr;
     size_t wave_trace_bytes = 0;
     int wave_trace_n = 0;
+    int phase_trace_n = 0;  // waves with a phase trace (RT_OPT_WAVE_TRACE 2)
     int job_trace_n = 0;
     double create_ms[8] = {0};  // rt_create phases (rt_debug_create_ms)
     int built_on_gpu = 0, bvh2_nodes = 0, bvh2_depth = 0;
@@ -940,7 +941,7 @@ static int set_option_one(rt_ctx* c, int option, int value) {
             c->opt_refill = value;
             return RT_OK;
         case RT_OPT_WAVE_TRACE:
-            c->opt_wave_trace = value ? 1 : 0;
+            c->opt_wave_trace = value == 2 ? 2 : value ? 1 : 0;
             return RT_OK;
         case RT_OPT_FAN_CAP:
             if (value < 0 || value > 64) break;
@@ -1613,14 +1614,17 @@ static int launch_render(rt_ctx* c, KParams& K, hipStream_t st, int count_mode, 
             K.frame_slots = (int)slots;
         }
         if (c->opt_wave_trace) {
+            const size_t ph = c->opt_wave_trace == 2 ? (size_t)grid * RT_PHASE_EV * 2 : 0;  // phase trace words
             const int rc = ensure(c, &c->d_wave_trace, &c->wave_trace_bytes,
-                                  (size_t)grid * 8 * 8 + (size_t)J.njobs * 3 * 8);
+                                  (size_t)grid * 8 * 8 + (size_t)J.njobs * 3 * 8 + ph * 8);
             if (rc != RT_OK) return rc;
             K.wave_trace = reinterpret_cast<unsigned long long*>(c->d_wave_trace);
             K.job_trace = K.wave_trace + (size_t)grid * 8;
-            HIP_TRY(hipMemsetAsync(K.job_trace, 0, (size_t)J.njobs * 3 * 8, st));
+            K.phase_trace = ph ? K.job_trace + (size_t)J.njobs * 3 : nullptr;
+            HIP_TRY(hipMemsetAsync(K.job_trace, 0, ((size_t)J.njobs * 3 + ph) * 8, st));
             c->wave_trace_n = grid;
             c->job_trace_n = J.njobs;
+            c->phase_trace_n = ph ? grid : 0;
         }
         HIP_TRY(hipEventRecord(c->ev0, st));
         const int lrc = count_mode ? launch_persistent<true>(grid, st, K, J, c) : launch_persistent<false>(grid, st, K, J, c);
@@ -2155,6 +2159,17 @@ extern "C" int rt_debug_job_trace(rt_ctx* c, uint64_t* out, int max_jobs) {
     if (n > 0)
         HIP_TRY(hipMemcpy(out, reinterpret_cast<unsigned long long*>(c->d_wave_trace) + (size_t)c->wave_trace_n * 8,
                           (size_t)n * 3 * 8, hipMemcpyDeviceToHost));
+    return n;
+}
+
+extern "C" int rt_debug_phase_trace(rt_ctx* c, uint64_t* out, int max_waves) {
+    if (!c || !out || max_waves <= 0) return RT_ERR_INVALID;
+    const int n = std::min(max_waves, c->phase_trace_n);
+    if (n > 0)
+        HIP_TRY(hipMemcpy(out,
+                          reinterpret_cast<unsigned long long*>(c->d_wave_trace) + (size_t)c->wave_trace_n * 8 +
+                              (size_t)c->job_trace_n * 3,
+                          (size_t)n * RT_PHASE_EV * 2 * 8, hipMemcpyDeviceToHost));
     return n;
 }
 

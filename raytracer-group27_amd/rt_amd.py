@@ -134,7 +134,7 @@ EXPORTS = [
     "rt_destroy", "rt_render", "rt_render_device", "rt_render_views_device", "rt_render_views", "rt_unpermute_bands_device", "rt_intersect", "rt_shade",
     "rt_set_counting", "rt_debug_counters", "rt_ctx_info", "rt_selftest_math",
     "rt_postprocess_device", "rt_bitmap_device", "rt_postprocess", "rt_bitmap", "rt_encode_bmp", "rt_write_bmp",
-    "rt_philox4x32_10", "rt_debug_wave_trace", "rt_debug_job_trace", "rt_debug_create_ms", "rt_set_build_mode", "rt_debug_build_info", "rt_debug_records", "rt_debug_ref_bvh", "rt_decode_png", "rt_ctx_set_option", "rt_texture_sample",
+    "rt_philox4x32_10", "rt_debug_wave_trace", "rt_debug_job_trace", "rt_debug_phase_trace", "rt_debug_create_ms", "rt_set_build_mode", "rt_debug_build_info", "rt_debug_records", "rt_debug_ref_bvh", "rt_decode_png", "rt_ctx_set_option", "rt_texture_sample",
     "rt_update_lights", "rt_update_materials", "rt_unpermute_views_device", "rt_scene_mesh_count", "rt_scene_mesh_get",
     "rt_ctx_devices", "rt_ctx_peer_stores", "rt_render_views_image_device", "rt_ipc_alloc", "rt_ipc_open", "rt_ipc_close", "rt_device_free",
     "rt_device_synchronize", "rt_memcpy_dtoh", "rt_debug_slab_check", "rt_source_hash",
@@ -328,6 +328,7 @@ def lib():
                               C.c_int),
             "rt_debug_wave_trace": ([vp, P(C.c_uint64), C.c_int], C.c_int),
             "rt_debug_job_trace": ([vp, P(C.c_uint64), C.c_int], C.c_int),
+            "rt_debug_phase_trace": ([vp, P(C.c_uint64), C.c_int], C.c_int),
             "rt_debug_create_ms": ([vp, P(C.c_double), C.c_int], C.c_int),
             "rt_set_build_mode": ([C.c_int], C.c_int),
             "rt_debug_build_info": ([vp, P(C.c_int), C.c_int], C.c_int),

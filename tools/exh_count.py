@@ -13,6 +13,7 @@ cfg = sys.argv[1] if len(sys.argv) > 1 else "C3"
 views = int(sys.argv[2]) if len(sys.argv) > 2 else 1
 s, p, W, H, desc = R.build_config(cfg)
 ctx = R.Context(s)
+ctx.set_option(R.OPT_WAVE_TRACE, 1)  # the per-query counters are kept only with the wave trace on
 R.lib().rt_set_counting(1)
 if views == 1:
     _, st = ctx.render(R.camera_from_trackball(aspect=R.aspect_of(W, H)), p, W, H)
