@@ -106,6 +106,8 @@ struct KParams {
     int interleave;             // job -> pixel: 0 a wave's 64 jobs are one 8x8 tile; k > 0 they spread over 2^k tiles
     int interleave_view;        // ... in the views from this one on (a batch's last views: its drain)
     int centre_first;           // job -> tile: the upper half's per-XCD tile ranges walked bottom-up (single frames)
+    int prio_iters;             // opaque kernel: a traversal phase raises its wave's issue priority after this many
+                                // iterations (0: never)
     int fan_cap;                // ... a wave with this many pixels waiting on fans takes no new pixels
     int dual;                   // dynamic-fetch kernel: a lane testing a leaf's records also visits its next node
     uint32_t seed_lo, seed_hi;  // glossy sampling: Philox-4x32-10 key (rt_params.rng_seed)

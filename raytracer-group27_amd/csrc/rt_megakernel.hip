@@ -2629,6 +2629,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
                     L.job = job_k;
                     uint32_t rpix;
                     if (job_pixel(P, job_k, rpix, out_row)) {
+                        if (COUNT && P.job_trace) P.job_trace[3 * job_k + 2] = rpix;  // the job's pixel id y * W + x
                         L.sample = 0;
                         camera_query(P, job_k, rpix, 0, q);
                         L.level = 0;
@@ -2700,8 +2701,11 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
             t_ph = wall_clock64();
             ntr_ph = (uint32_t)__popcll(__ballot(tracing));
         }
+        int it_prio = 0;  // (wave-uniform) this phase's iterations, for P.prio_iters
         for (;;) {
             if (COUNT && P.phase_trace) ++it_ph;
+            // a phase still tracing after prio_iters iterations holds the wave's slowest queries: issue first
+            if (P.prio_iters > 0 && ++it_prio == P.prio_iters) __builtin_amdgcn_s_setprio(2);
             if (COUNT) {
                 const int ntr = __popcll(__ballot(tracing));
                 if (wave_leader()) cnt.hist[min((ntr - 1) >> 4, 2)]++;
@@ -2799,6 +2803,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
             }
             if (COUNT && P.wave_trace) coop_n++;
         }
+        if (P.prio_iters > 0 && it_prio >= P.prio_iters) __builtin_amdgcn_s_setprio(0);
         if (COUNT && P.phase_trace) {
             if (lane_id == 0 && nph < RT_PHASE_EV) {
                 unsigned long long* w = P.phase_trace + ((size_t)blockIdx.x * RT_PHASE_EV + nph) * 2;

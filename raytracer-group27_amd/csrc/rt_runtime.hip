@@ -171,6 +171,7 @@ struct rt_ctx {
     int wf_trace_blocks[12] = {0};  // resident blocks of the trace kernel's builds (plain, counting)
     int opt_wf_build = 0;          // RT_OPT_WF_BUILD
     int opt_wf_streams = 0;        // RT_OPT_WF_STREAMS (0: RT_WF_STREAMS)
+    int opt_prio = -1;             // RT_OPT_PRIO (-1: by render shape)
     hipStream_t wf_streams[4] = {nullptr, nullptr, nullptr, nullptr};  // the chunks' extra streams ([0] unused)
     hipEvent_t wf_done[4] = {nullptr, nullptr, nullptr, nullptr};
 };
@@ -995,6 +996,10 @@ static int set_option_one(rt_ctx* c, int option, int value) {
             if (value < 0 || value > 4) break;
             c->opt_wf_streams = value;
             return RT_OK;
+        case RT_OPT_PRIO:
+            if (value < -1 || value > 100000) break;
+            c->opt_prio = value;
+            return RT_OK;
         default:
             set_error("rt_ctx_set_option: unknown option");
             return RT_ERR_INVALID;
@@ -1369,6 +1374,10 @@ static void shape_options(const rt_ctx* c, KParams& K) {
         K.coop = 2;
     }
     if (c->opt_refill > 0) K.refill = c->opt_refill;
+    // single frames: the waves whose phase is still tracing after 16 iterations issue first, so the frame's longest
+    // query chains run ahead of fresh work (C3 frame 0.951-0.968 -> 0.904-0.937 ms; batches neutral, 0.374-0.377 vs
+    // 0.376 ms/frame: profiles/r05/ab_r05z6_prio.log, ab_r05z7_prio.log, ab_r05z8_prio.log)
+    K.prio_iters = c->opt_prio >= 0 ? c->opt_prio : (K.n_views <= 1 ? 16 : 0);
     if (c->opt_coop >= 0) K.coop = c->opt_coop;
     if (c->opt_coop_max > 0) K.coop_max = std::min(K.coop_max, c->opt_coop_max);
     if (K.coop_max <= 0) K.coop = 0;

@@ -160,6 +160,7 @@ OPT_PEER_STORES = 14  # split renders: -1 peer stores where peer access works (d
 OPT_TREE = 13  # recursion-tree kernel (C4 / C5 class): -1 / 2 where eligible (default), 0 the general kernels, 1 its re-visit group stack build (A/B), 3 a checked 4-wave build
 OPT_INTERLEAVE_TAIL = 15  # opaque batches: the last n views interleaved over 16 tiles (0 none)
 OPT_WF_STREAMS = 18  # wavefront chunks over 1..4 streams (0: default 2)
+OPT_PRIO = 19  # opaque kernel: s_setprio 2 after this many iterations of a traversal phase (-1 by shape, 0 never)
 OPT_WF_BUILD = 17  # wavefront trace kernel build: 0 5 waves (default), 1 6, 2 4 + node prefetch, 3 8
 OPT_WAVEFRONT = 16  # opaque-kernel renders, one sample per pixel: -1 by shape, 0 the megakernel, 1 the wavefront path, 2..32 its refill
 KERNEL_AUTO, KERNEL_WHOLE_TRAVERSAL, KERNEL_DYNAMIC_FETCH = 0, 1, 2

@@ -55,3 +55,42 @@ for w in order[:show]:
     for k in np.nonzero(m)[0]:
         print(f"   phase {k:3d}: {start[w, k]:8.1f} .. {end[w, k]:8.1f} us ({dur[w, k]:7.1f}) tracing {ntr[w, k]:2d} "
               f"iters {iters[w, k]:4d}{' lane groups' if coop[w, k] else ''}")
+
+# the jobs that finished last: where they are in the image (job trace word 2 = the pixel id y * W + x)
+nj = 1 << 23
+jt = np.zeros(3 * nj, np.uint64)
+nj = R.lib().rt_debug_job_trace(ctx.h, jt.ctypes.data_as(C.POINTER(C.c_uint64)), nj)
+jt = jt[:3 * nj].reshape(nj, 3).astype(np.int64)
+done = jt[:, 1] > 0
+js = (jt[done, 0] - t0) / 100.0
+je = (jt[done, 1] - t0) / 100.0
+pix = jt[done, 2] % (W * H)
+py, px = pix // W, pix % W
+print("job start us pct (0 50 90 99 100):", np.percentile(js, [0, 50, 90, 99, 100]).round(1).tolist())
+print("job latency us pct (0 50 90 99 99.9 100):", np.percentile(je - js, [0, 50, 90, 99, 99.9, 100]).round(1).tolist())
+late = np.argsort(-je)[:2000]
+print(f"the 2000 last jobs: start us pct {np.percentile(js[late], [0, 50, 100]).round(1).tolist()}, latency pct "
+      f"{np.percentile((je - js)[late], [0, 50, 100]).round(1).tolist()}")
+# coarse map (12 x 8 cells): mean job latency, and the share of the last 2000 jobs
+gy, gx = 8, 12
+cy, cx = py * gy // H, px * gx // W
+lat = je - js
+print("mean job latency (us) by image cell (y up: row 0 = bottom of the frame):")
+for r in range(gy - 1, -1, -1):
+    row = []
+    for c in range(gx):
+        m = (cy == r) & (cx == c)
+        row.append(f"{lat[m].mean():6.0f}" if m.any() else "     -")
+    print("  " + " ".join(row))
+print("cells of the 2000 last jobs (count):")
+cnt = np.zeros((gy, gx), int)
+np.add.at(cnt, (cy[late], cx[late]), 1)
+for r in range(gy - 1, -1, -1):
+    print("  " + " ".join(f"{v:6d}" for v in cnt[r]))
+print("mean job start (us) by cell:")
+for r in range(gy - 1, -1, -1):
+    row = []
+    for c in range(gx):
+        m = (cy == r) & (cx == c)
+        row.append(f"{js[m].mean():6.0f}" if m.any() else "     -")
+    print("  " + " ".join(row))
