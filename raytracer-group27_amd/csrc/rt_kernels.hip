@@ -387,12 +387,18 @@ __device__ __forceinline__ bool sphere_test(const DSph& s, v3 o, v3 d, float& t_
     return false;
 }
 
+// The direction's reciprocals for the BVH8 slab tests, which only cull: every box is inflated by eps =
+// max(8, max |coordinate|) * 2^-16 (bvh_build.cpp, rt_build.hip), so a point the reference's triangle test
+// accepts lies >= eps * |inv| inside every slab interval in t, while a reciprocal off by 1 ulp moves each slab
+// t by <= 2^-23 |t| <= 2^-23 * (scene extent + origin distance) * |inv|: ~100x inside the margin, and the signs
+// (near / far plane choice) are exact.  So v_rcp_f32 (1 ulp) replaces the IEEE division's ~10-instruction
+// sequence per axis with the same culling outcome for every accepted candidate.
 __device__ __forceinline__ v3 safe_inv(v3 d) {
     const float e = 1e-20f;
     const float x = fabsf(d.x) < e ? copysignf(e, d.x) : d.x;
     const float y = fabsf(d.y) < e ? copysignf(e, d.y) : d.y;
     const float z = fabsf(d.z) < e ? copysignf(e, d.z) : d.z;
-    return v3{1.0f / x, 1.0f / y, 1.0f / z};
+    return v3{__builtin_amdgcn_rcpf(x), __builtin_amdgcn_rcpf(y), __builtin_amdgcn_rcpf(z)};
 }
 
 // HitInfo for the winner: hitPoint, normal (interpolated + flipped), material, uv.
