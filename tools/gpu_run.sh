@@ -62,6 +62,7 @@ for step in "$@"; do
     wave)  run 300 wave_${TAG}${c:+_count}.log env WT_VIEWS=${b:-1} WT_COUNT=${c:-0} python tools/wave_trace.py ${a:-C3} ;;
     jobs)  run 300 jobs_${TAG}${b:+_$b}.log python tools/job_trace.py ${a:-C3} ${b//;/ } ;;
     ranks) run 600 ranks_${TAG}.json env BENCH_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29555 bench.py --gpus 2 --steps 5 --warmup 1 --no-single-frame ;;
+    ranksv) run 600 ranks_${TAG}_v${a:-96}.json env BENCH_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29556 bench.py --gpus 2 --steps 3 --warmup 1 --no-single-frame --no-pmc --no-cpu-baseline --views ${a:-96} ;;
     ipc)   run 150 ipc_${TAG}_v${a:-96}.log python -u tools/ipc_probe.py --views ${a:-96} --timeout 110 ;;
     phases) run 200 phases_${TAG}_${a:-C3}_${b:-1}.log python -u tools/phase_trace.py ${a:-C3} ${b:-1} ${c:-6} ;;
     exh)   run 200 exh_${TAG}_${a:-C3}_${b:-1}.log python -u tools/exh_count.py ${a:-C3} ${b:-1} ;;
