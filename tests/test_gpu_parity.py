@@ -460,6 +460,34 @@ def test_bench_step_c3_64_views(R, O, ctxs):
     assert float(np.max(np.abs(view[xy[:, 1], xy[:, 0]] - ref))) <= TOL
 
 
+@pytest.mark.gpu
+def test_split_single_spot_light(R, O):
+    """SPLIT (rt_megakernel.hip split_node) with its one light a spot light: split_light's cone test decides
+    whether a node posts a segment (inside the cone) or keeps a zero colour (outside, src/shadow.cpp:235-237).  The
+    dragon proxy lit by one narrow spot light only, every SPLIT build against the general kernels, the opaque
+    kernel without SPLIT and the oracle (bits, ray count)."""
+    scene, prm, _, _, _ = R.build_config("C3", dragon_uv=(200, 80))
+    scene.clear_lights()
+    scene.add_spot_light((1, 1, -1), (-1, -1, 1), 15, (0.9, 0.7, 0.5))
+    W, H = 96, 54
+    ctx = R.Context(scene)
+    try:
+        cam = R.camera_from_trackball(aspect=R.aspect_of(W, H))
+        ref, rays = O.Oracle(scene).render(prm, W, H)
+        base = None
+        for opaque in (0, 1, 4, 5, 7):
+            with V.options(R, ctx, {R.OPT_KERNEL: R.KERNEL_DYNAMIC_FETCH, R.OPT_OPAQUE: opaque}):
+                img, st = ctx.render(cam, prm, W, H)
+            assert st.rays == rays, opaque
+            assert float(np.max(np.abs(img - ref))) <= TOL, opaque
+            if base is None:
+                base = img
+            assert img.tobytes() == base.tobytes(), opaque
+        assert float(np.abs(ref).max()) > 0.0  # the cone lights part of the object
+    finally:
+        ctx.close()
+
+
 def test_opaque_kernel_spot_lights(R, O):
     """Spot lights through the opaque-scene kernel (lite_next_light's cone test and its point-then-spot
     light order, rt_megakernel.hip) against the general kernels and the oracle: the dragon proxy lit by one
