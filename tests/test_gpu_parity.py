@@ -460,6 +460,35 @@ def test_bench_step_c3_64_views(R, O, ctxs):
     assert float(np.max(np.abs(view[xy[:, 1], xy[:, 0]] - ref))) <= TOL
 
 
+@pytest.mark.parametrize("depth,multi", [(0, 0), (9, 0), (4, 4)])
+def test_split_depths_and_samples(R, O, depth, multi):
+    """SPLIT at the recursion depths its frame and LDS result bits span (a lone level-0 node; ten levels) and with
+    getPixelRays' 4 samples per pixel (each sample folded and stored in sample order, store_sample): the SPLIT
+    builds against the opaque kernel without SPLIT and the oracle (bits, ray count)."""
+    scene, prm, _, _, _ = R.build_config("C3", dragon_uv=(200, 80))
+    prm = type(prm).from_buffer_copy(prm)
+    prm.max_reflection_level = depth
+    if multi:
+        prm.multiple_rays = 1
+        prm.sample_size = multi
+    W, H = 64, 36
+    ctx = R.Context(scene)
+    try:
+        cam = R.camera_from_trackball(aspect=R.aspect_of(W, H))
+        ref, rays = O.Oracle(scene).render(prm, W, H)
+        base = None
+        for opaque in (1, 4, 5):
+            with V.options(R, ctx, {R.OPT_KERNEL: R.KERNEL_DYNAMIC_FETCH, R.OPT_OPAQUE: opaque}):
+                img, st = ctx.render(cam, prm, W, H)
+            assert st.rays == rays, opaque
+            assert float(np.max(np.abs(img - ref))) <= TOL, opaque
+            if base is None:
+                base = img
+            assert img.tobytes() == base.tobytes(), opaque
+    finally:
+        ctx.close()
+
+
 @pytest.mark.gpu
 def test_split_single_spot_light(R, O):
     """SPLIT (rt_megakernel.hip split_node) with its one light a spot light: split_light's cone test decides
