@@ -1,0 +1,85 @@
+// Developer probe (not part of the library): what a divergent gather costs the vector memory pipe.
+// Each wave runs `iters` steps; in a step the lanes below `active` load one 128-B "node" (8 x dwordx4, as
+// node_fetch does) from a pseudo-random line of a buffer of `bytes`, the next line depending on the data
+// (a dependent walk, like a traversal).  Time per step against the active lane count shows whether the
+// memory pipe's cost follows the active lanes or the instruction.
+// Build: hipcc --offload-arch=gfx950 -O3 -o tools/td_probe tools/td_probe.hip
+// Run:   tools/td_probe [blocks] [iters]
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CHECK(x)                                                                      \
+    do {                                                                              \
+        hipError_t e_ = (x);                                                          \
+        if (e_ != hipSuccess) {                                                       \
+            std::fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));              \
+            std::exit(1);                                                             \
+        }                                                                             \
+    } while (0)
+
+__global__ __launch_bounds__(64) void walk(const float4* __restrict__ buf, unsigned nlines, int iters, int active,
+                                           float* out) {
+    const int lane = threadIdx.x;
+    unsigned line = (blockIdx.x * 64u + (unsigned)lane) * 2654435761u % nlines;
+    float acc = 0.0f;
+    if (lane < active) {
+        for (int i = 0; i < iters; ++i) {
+            const float4* p = buf + (size_t)line * 8;
+            float4 g[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) g[k] = p[k];
+            float s = 0.0f;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) s += g[k].x + g[k].y + g[k].z + g[k].w;
+            acc += s;
+            // the next line depends on the loaded data (a dependent walk); the data are small integers
+            line = (line * 1103515245u + 12345u + (unsigned)s) % nlines;
+        }
+    }
+    out[blockIdx.x * 64 + lane] = acc;
+}
+
+int main(int argc, char** argv) {
+    const int blocks = argc > 1 ? std::atoi(argv[1]) : 4096;
+    const int iters = argc > 2 ? std::atoi(argv[2]) : 2000;
+    const size_t sizes[] = {16u << 10, 2u << 20, 64u << 20, 1024u << 20};
+    const int actives[] = {64, 32, 16, 8, 1};
+    float4* buf;
+    float* out;
+    const size_t maxb = sizes[3];
+    CHECK(hipMalloc(&buf, maxb));
+    CHECK(hipMemset(buf, 0, maxb));
+    CHECK(hipMalloc(&out, (size_t)blocks * 64 * sizeof(float)));
+    hipEvent_t a, b;
+    CHECK(hipEventCreate(&a));
+    CHECK(hipEventCreate(&b));
+    std::printf("blocks %d, iters %d: ns per wave step (one 128-B node per active lane)\n", blocks, iters);
+    std::printf("%12s", "buffer");
+    for (int act : actives) std::printf("  active %2d", act);
+    std::printf("   (lines/us chip-wide at 64 | at 8)\n");
+    for (size_t bytes : sizes) {
+        const unsigned nlines = (unsigned)(bytes / 128);
+        std::printf("%10zu K", bytes >> 10);
+        double t64 = 0, t8 = 0;
+        for (int act : actives) {
+            hipLaunchKernelGGL(walk, dim3(blocks), dim3(64), 0, 0, buf, nlines, iters / 10, act, out);  // warm
+            CHECK(hipEventRecord(a));
+            hipLaunchKernelGGL(walk, dim3(blocks), dim3(64), 0, 0, buf, nlines, iters, act, out);
+            CHECK(hipEventRecord(b));
+            CHECK(hipEventSynchronize(b));
+            CHECK(hipGetLastError());
+            float ms = 0;
+            CHECK(hipEventElapsedTime(&ms, a, b));
+            const double ns_step = ms * 1e6 / iters;  // every wave runs `iters` steps concurrently
+            if (act == 64) t64 = (double)blocks * 64 * iters / (ms * 1e3);
+            if (act == 8) t8 = (double)blocks * 8 * iters / (ms * 1e3);
+            std::printf("  %9.1f", ns_step);
+        }
+        std::printf("   (%.0f | %.0f)\n", t64, t8);
+    }
+    CHECK(hipFree(buf));
+    CHECK(hipFree(out));
+    return 0;
+}
