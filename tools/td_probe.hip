@@ -41,6 +41,40 @@ __global__ __launch_bounds__(64) void walk(const float4* __restrict__ buf, unsig
     out[blockIdx.x * 64 + lane] = acc;
 }
 
+// The same walk with the nodes gathered cooperatively: gather k has lane i fetch 16-B chunk (i & 7) of the node
+// of lane 8k + (i >> 3) into LDS, so one instruction touches 8 lines instead of 64, and a wave with A active
+// lanes issues ceil(A / 8) gathers instead of 8; each lane then reads its own node back (8 x ds_read_b128).
+__global__ __launch_bounds__(64) void walk_coop(const float4* __restrict__ buf, unsigned nlines, int iters, int active,
+                                                float* out) {
+    __shared__ float4 st[64 * 8];
+    const int lane = threadIdx.x;
+    unsigned line = (blockIdx.x * 64u + (unsigned)lane) * 2654435761u % nlines;
+    float acc = 0.0f;
+    const int ngather = (active + 7) >> 3;
+    for (int i = 0; i < iters; ++i) {
+        for (int k = 0; k < ngather; ++k) {
+            const int src = 8 * k + (lane >> 3);
+            const unsigned l = (unsigned)__shfl((int)line, src);
+            if (src < active) st[src * 8 + (lane & 7)] = buf[(size_t)l * 8 + (lane & 7)];
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (lane < active) {
+            float s = 0.0f;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const float4 g = st[lane * 8 + k];
+                s += g.x + g.y + g.z + g.w;
+            }
+            acc += s;
+            line = (line * 1103515245u + 12345u + (unsigned)s) % nlines;
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+    out[blockIdx.x * 64 + lane] = acc;
+}
+
 int main(int argc, char** argv) {
     const int blocks = argc > 1 ? std::atoi(argv[1]) : 4096;
     const int iters = argc > 2 ? std::atoi(argv[2]) : 2000;
@@ -56,17 +90,19 @@ int main(int argc, char** argv) {
     CHECK(hipEventCreate(&a));
     CHECK(hipEventCreate(&b));
     std::printf("blocks %d, iters %d: ns per wave step (one 128-B node per active lane)\n", blocks, iters);
-    std::printf("%12s", "buffer");
+    std::printf("%16s", "gather / buffer");
     for (int act : actives) std::printf("  active %2d", act);
     std::printf("   (lines/us chip-wide at 64 | at 8)\n");
+    for (int coop = 0; coop < 2; ++coop)
     for (size_t bytes : sizes) {
         const unsigned nlines = (unsigned)(bytes / 128);
-        std::printf("%10zu K", bytes >> 10);
+        std::printf("%s%10zu K", coop ? "coop" : "lane", bytes >> 10);
         double t64 = 0, t8 = 0;
         for (int act : actives) {
-            hipLaunchKernelGGL(walk, dim3(blocks), dim3(64), 0, 0, buf, nlines, iters / 10, act, out);  // warm
+            auto k = coop ? walk_coop : walk;
+            hipLaunchKernelGGL(k, dim3(blocks), dim3(64), 0, 0, buf, nlines, iters / 10, act, out);  // warm
             CHECK(hipEventRecord(a));
-            hipLaunchKernelGGL(walk, dim3(blocks), dim3(64), 0, 0, buf, nlines, iters, act, out);
+            hipLaunchKernelGGL(k, dim3(blocks), dim3(64), 0, 0, buf, nlines, iters, act, out);
             CHECK(hipEventRecord(b));
             CHECK(hipEventSynchronize(b));
             CHECK(hipGetLastError());
