@@ -44,6 +44,9 @@ __global__ __launch_bounds__(64) void walk(const float4* __restrict__ buf, unsig
 // The same walk with the nodes gathered cooperatively: gather k has lane i fetch 16-B chunk (i & 7) of the node
 // of lane 8k + (i >> 3) into LDS, so one instruction touches 8 lines instead of 64, and a wave with A active
 // lanes issues ceil(A / 8) gathers instead of 8; each lane then reads its own node back (8 x ds_read_b128).
+// SWZ: chunk c of node s sits at entry s * 8 + (c ^ (s & 7)), so the 8 lanes of a read-back quad-group hit 8
+// different bank groups (unswizzled, every lane's chunk k is in the same one)
+template <bool SWZ>
 __global__ __launch_bounds__(64) void walk_coop(const float4* __restrict__ buf, unsigned nlines, int iters, int active,
                                                 float* out) {
     __shared__ float4 st[64 * 8];
@@ -55,7 +58,8 @@ __global__ __launch_bounds__(64) void walk_coop(const float4* __restrict__ buf, 
         for (int k = 0; k < ngather; ++k) {
             const int src = 8 * k + (lane >> 3);
             const unsigned l = (unsigned)__shfl((int)line, src);
-            if (src < active) st[src * 8 + (lane & 7)] = buf[(size_t)l * 8 + (lane & 7)];
+            const int c = lane & 7;
+            if (src < active) st[src * 8 + (SWZ ? (c ^ (src & 7)) : c)] = buf[(size_t)l * 8 + c];
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -63,7 +67,7 @@ __global__ __launch_bounds__(64) void walk_coop(const float4* __restrict__ buf, 
             float s = 0.0f;
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
-                const float4 g = st[lane * 8 + k];
+                const float4 g = st[lane * 8 + (SWZ ? (k ^ (lane & 7)) : k)];
                 s += g.x + g.y + g.z + g.w;
             }
             acc += s;
@@ -93,13 +97,13 @@ int main(int argc, char** argv) {
     std::printf("%16s", "gather / buffer");
     for (int act : actives) std::printf("  active %2d", act);
     std::printf("   (lines/us chip-wide at 64 | at 8)\n");
-    for (int coop = 0; coop < 2; ++coop)
+    for (int coop = 0; coop < 3; ++coop)
     for (size_t bytes : sizes) {
         const unsigned nlines = (unsigned)(bytes / 128);
-        std::printf("%s%10zu K", coop ? "coop" : "lane", bytes >> 10);
+        std::printf("%s%10zu K", coop == 2 ? "cswz" : coop ? "coop" : "lane", bytes >> 10);
         double t64 = 0, t8 = 0;
         for (int act : actives) {
-            auto k = coop ? walk_coop : walk;
+            auto k = coop == 2 ? walk_coop<true> : coop ? walk_coop<false> : walk;
             hipLaunchKernelGGL(k, dim3(blocks), dim3(64), 0, 0, buf, nlines, iters / 10, act, out);  // warm
             CHECK(hipEventRecord(a));
             hipLaunchKernelGGL(k, dim3(blocks), dim3(64), 0, 0, buf, nlines, iters, act, out);
