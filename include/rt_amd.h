@@ -394,10 +394,11 @@ int rt_debug_counters(rt_ctx* ctx, uint64_t* out, int n);
 #define RT_OPT_TREE 13       /* recursion-tree kernel (transparent materials, all four light types with <= 64-sample fans, no lobes or textures): -1 / 2 where eligible, 0 never, 1 its build with the re-visit group stack (A/B), 3 a checked 4-wave build (developer diagnosis: out-of-range indices reported in rt_debug_counters [24] / [25] instead of accessed) */
 #define RT_OPT_PEER_STORES 14 /* split renders: -1 the replicas with peer access to devices[0] store their pixels straight into its images (default), 0 every replica renders band-dense on its own device and copies (the path of devices without peer access) */
 #define RT_OPT_INTERLEAVE_TAIL 15 /* opaque-kernel view batches: the last n views' jobs spread over 16 tiles per wave (the launch's drain), the others in tile order; 0 none (the default: measured slower) */
-#define RT_OPT_WAVEFRONT 16   /* opaque-kernel scenes with one camera sample per pixel: -1 by render shape (default), 0 the persistent opaque megakernel, 1 the wavefront path (rt_wavefront.hip: a lean trace kernel per recursion level and an elementwise shade kernel between; bit-identical images), 2..64 the wavefront path with this trace-kernel refill threshold (A/B) */
+#define RT_OPT_WAVEFRONT 16   /* opaque-kernel scenes with one camera sample per pixel: -1 (default) and 0 the persistent opaque megakernel (no render shape is faster on the wavefront path), 1 the wavefront path (rt_wavefront.hip: a lean trace kernel per recursion level and an elementwise shade kernel between; bit-identical images), 2..64 the wavefront path with this trace-kernel refill threshold (A/B) */
 #define RT_OPT_WF_BUILD 17   /* wavefront trace kernel build (A/B): 0 5 waves per SIMD (default), 1 6 waves, 2 4 waves with the node prefetch, 3 8 waves, 4 5 waves with a dual step's node and record loads in flight together, 5 the same at 4 waves */
 #define RT_OPT_WF_STREAMS 18 /* wavefront path: streams its chunks of camera jobs are spread over (0: 2, the default; 1..4), so one chunk's small recursion levels overlap another's busy ones */
 #define RT_OPT_PRIO 19       /* opaque-scene kernel: a traversal phase raises its wave's issue priority (s_setprio 2) after this many iterations, so the waves holding the slowest queries issue first (-1 by render shape, 0 never) */
+#define RT_OPT_WF_CHUNK 20   /* wavefront path: camera jobs per chunk at most, a multiple of 64 (0: the memory budget's, the default; chunks are also capped below 2^27 jobs, the segment tag's shading-point field) */
 #define RT_KERNEL_AUTO 0
 #define RT_KERNEL_WHOLE_TRAVERSAL 1
 #define RT_KERNEL_DYNAMIC_FETCH 2

@@ -37,8 +37,21 @@ def _sources():
     return out
 
 
+def _toolchain():
+    """What besides the sources decides the code: the offload arch, the hipcc path and the ROCm release
+    (read from /opt/rocm/.info/version, no subprocess), so a library built for another arch or toolchain
+    does not pass for this tree's."""
+    try:
+        with open(os.path.join(os.path.dirname(os.path.dirname(os.path.realpath(HIPCC))), ".info", "version")) as f:
+            rel = f.read().strip()
+    except OSError:
+        rel = ""
+    return f"arch={ARCH};hipcc={HIPCC};rocm={rel}"
+
+
 def source_hash(defines=()):
-    """SHA-256 (16 hex digits) of the library's sources: each file's name and bytes, then any -D defines."""
+    """SHA-256 (16 hex digits) of the library's sources: each file's name and bytes, then any -D defines,
+    then the toolchain (_toolchain)."""
     h = hashlib.sha256()
     for name, path in _sources():
         with open(path, "rb") as f:
@@ -46,6 +59,7 @@ def source_hash(defines=()):
         h.update(name.encode() + b"\0" + str(len(data)).encode() + b"\0" + data)
     for d in defines:
         h.update(b"-D" + d.encode() + b"\0")
+    h.update(_toolchain().encode())
     return h.hexdigest()[:16]
 
 

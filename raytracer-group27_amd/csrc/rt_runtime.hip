@@ -106,7 +106,7 @@ struct rt_ctx {
     bool df_ok = true;  // the BVH8 fits the dynamic-fetch kernel's LDS stack
     bool glossy_material = false;  // opaque, ks > 0, shininess != 0 (glossy_ray_count > 1 draws lobes)
     int persistent_blocks[1024] = {0};  // resident 64-lane blocks per (kernel class, variant)
-    int opaque_blocks[6] = {0, 0, 0, 0, 0, 0};  // ... of the opaque-scene kernel (4 / 3 waves per SIMD; SPLIT; A/Bs)
+    int opaque_blocks[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // ... of the opaque-scene kernel (4 / 3 waves per SIMD; SPLIT; A/Bs)
     int tree_blocks[3] = {0, 0, 0};     // ... of the recursion-tree kernel (3-wave, re-visit, checked 4-wave)
     // recursion-tree kernel: the lanes' pending refracted rays (KParams::frames)
     float* d_frames = nullptr;
@@ -173,6 +173,9 @@ struct rt_ctx {
     int opt_wf_build = 0;          // RT_OPT_WF_BUILD
     int opt_wf_streams = 0;        // RT_OPT_WF_STREAMS (0: RT_WF_STREAMS)
     int opt_prio = -1;             // RT_OPT_PRIO (-1: by render shape)
+    int opt_wf_chunk = 0;          // RT_OPT_WF_CHUNK: camera jobs per wavefront chunk at most (0: the memory budget's)
+    const void* wf_last_cnt = nullptr;  // the WfCnt of the stream set that ran the last render's last wavefront chunk
+                                        // (nullptr: the last render took a megakernel; rt_debug_counters)
     hipStream_t wf_streams[4] = {nullptr, nullptr, nullptr, nullptr};  // the chunks' extra streams ([0] unused)
     hipEvent_t wf_done[4] = {nullptr, nullptr, nullptr, nullptr};
 };
@@ -972,7 +975,7 @@ static int set_option_one(rt_ctx* c, int option, int value) {
             c->opt_variant = value;
             return RT_OK;
         case RT_OPT_OPAQUE:
-            if (value < -1 || value > 7) break;
+            if (value < -1 || value > 9) break;
             c->opt_opaque = value;
             return RT_OK;
         case RT_OPT_TREE:
@@ -1002,6 +1005,10 @@ static int set_option_one(rt_ctx* c, int option, int value) {
         case RT_OPT_PRIO:
             if (value < -1 || value > 100000) break;
             c->opt_prio = value;
+            return RT_OK;
+        case RT_OPT_WF_CHUNK:
+            if (value < 0 || (value & 63)) break;
+            c->opt_wf_chunk = value;
             return RT_OK;
         default:
             set_error("rt_ctx_set_option: unknown option");
@@ -1080,7 +1087,11 @@ static bool opaque_path(const rt_ctx* c, const KParams& K, bool pixels) {
 #define RT_OPAQUE_V5S (RT_V_W5 | RT_V_NOPF | RT_V_NOCOOP | RT_V_SPLIT)   // A/B: 5 waves, no drain lane groups
 #define RT_OPAQUE_V4SN (RT_V_W4 | RT_V_NOPF | RT_V_NOCOOP | RT_V_SPLIT)  // A/B: 4 waves, no drain lane groups
 static bool split_ok(const KParams& K) { return K.S.npl + K.S.nspot == 1 && K.max_level < 16; }
+#define RT_OPAQUE_VG (RT_OPAQUE_V | RT_V_GLDS)  // the visitors' nodes by LDS-DMA (node_stage_glds)
+#define RT_OPAQUE_VG3S (RT_OPAQUE_V3 | RT_V_GLDS | RT_V_SPLIT)  // ... at 3 waves, every lane's node staged
 static int opaque_variant(const rt_ctx* c, const KParams& K) {
+    if (c->opt_opaque == 8) return split_ok(K) ? (RT_OPAQUE_VG | RT_V_SPLIT) : RT_OPAQUE_VG;
+    if (c->opt_opaque == 9 && split_ok(K)) return RT_OPAQUE_VG3S;
     if (c->opt_opaque == 2) return RT_OPAQUE_V3;
     if (c->opt_opaque == 3) return RT_OPAQUE_V | RT_V_REVISIT;
     if (c->opt_opaque == 1 || !split_ok(K)) return RT_OPAQUE_V;
@@ -1156,6 +1167,12 @@ static int launch_persistent(int grid, hipStream_t st, const KParams& K, const J
             hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V5S>), dim3(grid), dim3(64), 0, st, K, J);
         } else if (v == RT_OPAQUE_V4SN) {
             hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V4SN>), dim3(grid), dim3(64), 0, st, K, J);
+        } else if (v == (RT_OPAQUE_VG | RT_V_SPLIT)) {
+            hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_VG | RT_V_SPLIT>), dim3(grid), dim3(64), 0, st, K, J);
+        } else if (v == RT_OPAQUE_VG) {
+            hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_VG>), dim3(grid), dim3(64), 0, st, K, J);
+        } else if (v == RT_OPAQUE_VG3S) {
+            hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_VG3S>), dim3(grid), dim3(64), 0, st, K, J);
         } else {
             hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V>), dim3(grid), dim3(64), 0, st, K, J);
         }
@@ -1204,12 +1221,16 @@ static int occupancy_of(int* per_cu) {
 static int persistent_grid(rt_ctx* c, const KParams& K, bool pixels) {
     if (opaque_path(c, K, pixels)) {
         const int v = opaque_variant(c, K);
-        const int key = v == RT_OPAQUE_V5S ? 4 : v == RT_OPAQUE_V4SN ? 5 : ((v & RT_V_W3) ? 1 : 0) + ((v & RT_V_SPLIT) ? 2 : 0);
+        const int key = v == RT_OPAQUE_VG3S ? 8 : v == (RT_OPAQUE_VG | RT_V_SPLIT) ? 6 : v == RT_OPAQUE_VG ? 7 : v == RT_OPAQUE_V5S ? 4 : v == RT_OPAQUE_V4SN ? 5
+                      : ((v & RT_V_W3) ? 1 : 0) + ((v & RT_V_SPLIT) ? 2 : 0);
         if (c->opaque_blocks[key] > 0) return c->opaque_blocks[key];
         int cus = 0, per_cu = 0;
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
         const hipError_t e =
-            key == 5   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V4SN>, 64, 0)
+            key == 8   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_VG3S>, 64, 0)
+            : key == 7 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_VG>, 64, 0)
+            : key == 6 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_VG | RT_V_SPLIT>, 64, 0)
+            : key == 5 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V4SN>, 64, 0)
             : key == 4 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V5S>, 64, 0)
             : key == 3 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V3 | RT_V_SPLIT>, 64, 0)
             : key == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V | RT_V_SPLIT>, 64, 0)
@@ -1423,11 +1444,15 @@ static void shape_options(const rt_ctx* c, KParams& K) {
 
 // ---- the wavefront path (rt_wavefront.hip) ----
 // its scope: the opaque kernel's renders with one camera sample per pixel and at most 32 lights (one bit each)
-#define RT_WF_REFILL 16             // trace kernel: waiting lanes that take new queries together (RT_OPT_WAVEFRONT 2..32)
+#define RT_WF_REFILL 16             // trace kernel: waiting lanes that take new queries together (RT_OPT_WAVEFRONT 2..64)
+#ifndef RT_WF_MAX_CHUNK
+#define RT_WF_MAX_CHUNK ((1ll << 27) - 64)  // camera jobs per chunk at most (the segment tag's 27-bit shading point)
+#endif
 #define RT_WF_STREAMS 2       // streams the chunks of a large render are spread over (RT_OPT_WF_STREAMS)
 #define RT_WF_MAX_STREAMS 4
 #define RT_WF_BUDGET (64ull << 30)  // bytes of queues and shading points per chunk of camera jobs (at most; and
                                     // at most a third of the free HBM)
+// -1 (the default) is the megakernel: no render shape measured faster on the wavefront path
 static bool wf_path(const rt_ctx* c, const KParams& K) {
     if (c->opt_wavefront == 0 || !opaque_path(c, K, true) || K.aa || K.multi) return false;
     if (K.S.npl + K.S.nspot > 32) return false;
@@ -1500,6 +1525,10 @@ static int launch_wavefront(rt_ctx* c, KParams& K, hipStream_t st, rt_stats* sta
     const int nstreams = (int)std::max<long long>(
         1, std::min<long long>(want_streams, c->opt_wf_streams > 0 ? tiles : tiles / 1024));
     long long J = std::max<long long>(64, (long long)(budget / nstreams / per_job));  // jobs per chunk (at most)
+    // a segment's tag packs its shading point as h << 5 | light (rt_wavefront.hip): h < J must stay below 2^27, and
+    // below the EMPTY marker's (2^27 - 1, light 31)
+    J = std::min<long long>(J, RT_WF_MAX_CHUNK);
+    if (c->opt_wf_chunk > 0) J = std::min<long long>(J, c->opt_wf_chunk);
     long long nchunks = std::max<long long>(nstreams, (njobs + J - 1) / J);
     nchunks = (nchunks + nstreams - 1) / nstreams * nstreams;  // whole rounds of the streams
     J = ((njobs + nchunks - 1) / nchunks + 63) / 64 * 64;
@@ -1566,6 +1595,7 @@ static int launch_wavefront(rt_ctx* c, KParams& K, hipStream_t st, rt_stats* sta
         }
     }
     HIP_TRY(hipGetLastError());
+    c->wf_last_cnt = Bs[(int)((nchunks - 1) % nstreams)].cnt;
     for (int k = 1; k < nstreams; ++k) {
         HIP_TRY(hipEventRecord(c->wf_done[k], sts[k]));
         HIP_TRY(hipStreamWaitEvent(st, c->wf_done[k], 0));
@@ -1600,6 +1630,7 @@ static int launch_render(rt_ctx* c, KParams& K, hipStream_t st, int count_mode, 
     shape_options(c, K);
     if (blocks > 0 && wf_path(c, K))
         return count_mode ? launch_wavefront<true>(c, K, st, stats) : launch_wavefront<false>(c, K, st, stats);
+    c->wf_last_cnt = nullptr;
     HIP_TRY(hipMemsetAsync(c->d_stats, 0, RT_STATS_BYTES, st));
     if (blocks > 0) {
         JobSrc J{};
@@ -2147,9 +2178,13 @@ extern "C" int rt_debug_counters(rt_ctx* c, uint64_t* out, int n) {
     unsigned long long h[RT_STATS_EXTRA + 16] = {0};
     HIP_TRY(hipMemcpy(h, c->d_stats, sizeof(h), hipMemcpyDeviceToHost));
     for (int i = 0; i < n && i < 32; ++i) out[i] = h[i < 16 ? i : RT_STATS_EXTRA + i - 16];
-    if (n > 32 && c->d_wf) {  // [32 ..]: the last wavefront chunk's hits per level (WfCnt::hits)
+    // [32 ..]: the last wavefront chunk's hits per level (WfCnt::hits of the stream set that ran it); zero when
+    // the last render took a megakernel
+    for (int i = 32; i < n && i < 32 + RT_MAX_DEPTH + 2; ++i) out[i] = 0;
+    if (n > 32 && c->wf_last_cnt) {
         int wh[RT_MAX_DEPTH + 2] = {0};
-        HIP_TRY(hipMemcpy(wh, c->d_wf, sizeof(wh), hipMemcpyDeviceToHost));
+        HIP_TRY(hipDeviceSynchronize());  // the chunk's stream set is not ordered with the null stream's copy
+        HIP_TRY(hipMemcpy(wh, c->wf_last_cnt, sizeof(wh), hipMemcpyDeviceToHost));
         for (int i = 32; i < n && i < 32 + RT_MAX_DEPTH + 2; ++i) out[i] = (uint64_t)wh[i - 32];
     }
     return RT_OK;

@@ -7,7 +7,7 @@ import contextlib
 def defaults(R):
     return {R.OPT_KERNEL: R.KERNEL_AUTO, R.OPT_VARIANT: -1, R.OPT_COOP: -1, R.OPT_COOP_MAX: 0, R.OPT_REFILL: 0,
             R.OPT_FAN: 1, R.OPT_INTERLEAVE: -1, R.OPT_FAN_CAP: 0, R.OPT_DUAL_STEP: -1, R.OPT_OPAQUE: -1,
-            R.OPT_CENTRE_FIRST: -1, R.OPT_TREE: -1, R.OPT_INTERLEAVE_TAIL: 0, R.OPT_WAVEFRONT: -1, R.OPT_WF_BUILD: 0, R.OPT_WF_STREAMS: 0, R.OPT_PRIO: -1}
+            R.OPT_CENTRE_FIRST: -1, R.OPT_TREE: -1, R.OPT_INTERLEAVE_TAIL: 0, R.OPT_WAVEFRONT: -1, R.OPT_WF_BUILD: 0, R.OPT_WF_STREAMS: 0, R.OPT_PRIO: -1, R.OPT_WF_CHUNK: 0}
 
 
 def kernel_classes(R):
@@ -40,6 +40,7 @@ def all_variants(R):
         {R.OPT_KERNEL: df, R.OPT_OPAQUE: 4},                    # ... its 4-wave build, segments beside the mirror chain
         {R.OPT_KERNEL: df, R.OPT_OPAQUE: 5},                    # ... the same in the 3-wave build
         {R.OPT_KERNEL: df, R.OPT_OPAQUE: 7},                    # ... SPLIT without the drain lane groups
+        {R.OPT_KERNEL: df, R.OPT_OPAQUE: 8},                    # ... nodes staged by LDS-DMA (GLDS)
         {R.OPT_KERNEL: df, R.OPT_PRIO: 4},                      # ... issue priority after 4 iterations of a phase
         {R.OPT_KERNEL: df, R.OPT_REFILL: 32},                   # ... and a half-wave refill
         {R.OPT_KERNEL: df, R.OPT_COOP: 1},                      # ... drain lane groups in the drain only
@@ -57,6 +58,7 @@ def all_variants(R):
         {R.OPT_KERNEL: df, R.OPT_WAVEFRONT: 1, R.OPT_WF_STREAMS: 3},  # ... its chunks over three streams
         {R.OPT_KERNEL: df, R.OPT_WAVEFRONT: 1, R.OPT_WF_BUILD: 4},  # ... node and record loads of a step together
         {R.OPT_KERNEL: df, R.OPT_WAVEFRONT: 1, R.OPT_WF_BUILD: 5},  # ... the same at 4 waves
+        {R.OPT_KERNEL: df, R.OPT_WAVEFRONT: 1, R.OPT_WF_CHUNK: 128, R.OPT_WF_STREAMS: 3},  # ... 2-tile chunks (boundaries)
     ]
     return out
 

@@ -23,7 +23,7 @@ args = ap.parse_args()
 if args.lib:
     R.LIB_PATH = os.path.abspath(args.lib)
 
-DEFAULTS = {R.OPT_KERNEL: 0, R.OPT_VARIANT: -1, R.OPT_COOP: -1, R.OPT_COOP_MAX: 0, R.OPT_REFILL: 0, R.OPT_FAN: 1, R.OPT_INTERLEAVE: -1, R.OPT_FAN_CAP: 0, R.OPT_DUAL_STEP: -1, R.OPT_OPAQUE: -1, R.OPT_CENTRE_FIRST: -1, R.OPT_TREE: -1, R.OPT_INTERLEAVE_TAIL: 0, R.OPT_WAVEFRONT: -1, R.OPT_WF_BUILD: 0, R.OPT_WF_STREAMS: 0, R.OPT_PRIO: -1}
+DEFAULTS = {R.OPT_KERNEL: 0, R.OPT_VARIANT: -1, R.OPT_COOP: -1, R.OPT_COOP_MAX: 0, R.OPT_REFILL: 0, R.OPT_FAN: 1, R.OPT_INTERLEAVE: -1, R.OPT_FAN_CAP: 0, R.OPT_DUAL_STEP: -1, R.OPT_OPAQUE: -1, R.OPT_CENTRE_FIRST: -1, R.OPT_TREE: -1, R.OPT_INTERLEAVE_TAIL: 0, R.OPT_WAVEFRONT: -1, R.OPT_WF_BUILD: 0, R.OPT_WF_STREAMS: 0, R.OPT_PRIO: -1, R.OPT_WF_CHUNK: 0}
 
 
 def parse(a):
@@ -47,6 +47,7 @@ for cfg in args.configs:
     buf = torch.zeros(args.views * R.local_band_elems(W, H, 8, 1), dtype=torch.float32, device="cuda")
     res = {n: {"frame": [], "batch": []} for n, _ in arms}
     rays = {}
+    sums = {}
     for r in range(args.rounds + 1):
         for name, opts in arms:
             for k, v in DEFAULTS.items():
@@ -55,7 +56,11 @@ for cfg in args.configs:
                 ctx.set_option(k, v)
             st1 = ctx.render_device(cam, p, W, H, 8, 0, 1, buf.data_ptr(), None)
             stv = ctx.render_views_device(cams, p, W, H, 8, 0, 1, buf.data_ptr(), None) if args.views > 1 else st1
-            if r == 0:  # warm-up round
+            if r == 0:  # warm-up round: the rays and a checksum of the batch's bits (arms must agree)
+                torch.cuda.synchronize()
+                x = buf.view(torch.int32).to(torch.int64)
+                sums[name] = (int(x.sum()), int((x * x).sum()))
+                del x
                 rays[name] = (st1.rays, stv.rays, st1.kernel_name)
                 continue
             res[name]["frame"].append(st1.kernel_ms)
@@ -64,6 +69,8 @@ for cfg in args.configs:
         f = float(np.median(res[name]["frame"]))
         b = float(np.median(res[name]["batch"])) / args.views
         r1, rv, kn = rays[name]
+        same = "bits = arm 1" if sums[name] == sums[arms[0][0]] and rays[name][1] == rays[arms[0][0]][1] else \
+            "BITS DIFFER from arm 1"
         print(f"{cfg} {name:>10}: frame {f:7.3f} ms ({r1 / f / 1e3:7.1f} Mrays/s)  batch {b:7.3f} ms/frame "
-              f"({rv / args.views / b / 1e3:7.1f} Mrays/s)  [{kn}]", flush=True)
+              f"({rv / args.views / b / 1e3:7.1f} Mrays/s)  [{kn}] {same}", flush=True)
     ctx.close()
