@@ -42,9 +42,15 @@ VALU_PEAK_WAVE_INSTR_S = 256 * 4 * 2.4e9 / 2
 # the SQ counters of the issue / latency picture, one rocprofv3 pass (<= 8 SQ counters per pass)
 SQ_PASS = ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
            "SQ_BUSY_CYCLES")
+# the L2 hit rate of the same launches (2 TCC counters, a pass of its own: FETCH_SIZE already takes 3 of the 4)
+L2_PASS = ("TCC_HIT_sum", "TCC_MISS_sum")
+# cache-served gather rates chip-wide (MI355X_MICROARCH.md "Indexed rows: gather into LDS"): rows served by an XCD's
+# L2 16.8-18.8 TB/s, uniformly random rows of a 38 MB table (the Infinity Cache) 8.6 TB/s
+L2_GATHER_TBS = 17.8
+IC_GATHER_TBS = 8.6
 # BASELINE.md's full CPU sample (4 096 pixels of the seed-12345 permutation for C3-C5, whole frames for C1 / C2),
 # timed by tools/cpu_baseline.py on the GPU box's host; the bench line's own leg is a bounded prefix of it
-CPU_FULL = os.path.join("profiles", "r03", "cpu_baseline_full.json")
+CPU_FULL = os.path.join("profiles", "r06", "cpu_baseline_full.json")
 BAND_ROWS = 8
 DEFAULT_VIEWS = 64  # frames per step: a 64-view turntable (5.625 deg apart) of the C3 scene in one launch
 # frames per step of the other configs (a step of a few hundred ms at most): C4's 64-sample soft shadows
@@ -121,6 +127,7 @@ def cpu_baseline(config, budget_s=12.0, seed=12345, max_pixels=None):
             legs[key] = {"value": rays / dt / 1e6, "cores": threads, "pixels": npx, "rays": rays,
                          "seconds": round(dt, 2)}
     base = legs["1core_bvh0"]
+    whole = all(v["pixels"] == W * H for v in legs.values())
     full = None
     try:  # BASELINE.md's whole sample, timed once in full (tools/cpu_baseline.py) on the GPU box's host
         with open(os.path.join(REPO, CPU_FULL)) as f:
@@ -131,6 +138,12 @@ def cpu_baseline(config, budget_s=12.0, seed=12345, max_pixels=None):
                                          "seconds": v["seconds"]} for k, v in c["legs"].items()}}
     except (OSError, ValueError, KeyError):
         pass
+    if whole:
+        return {"value": base["value"], "unit": "Mrays/s", "cores": 1, "kind": "port",
+                "sample": f"BASELINE.md's sample for {config}: the whole {W}x{H} frame, {base['rays']} rays in "
+                          f"{base['seconds']} s single-threaded, useBVH=false (reference default); legs: 1 / {allc} "
+                          f"threads x useBVH false / true; host CPU: {_cpu_model()}",
+                "legs": legs}
     return {"value": base["value"], "unit": "Mrays/s", "cores": 1, "kind": "port",
             "sample": f"bounded prefix of BASELINE.md's sample (the first pixels of the seed-{seed} permutation of "
                       f"{config} {W}x{H}): {base['pixels']} pixels, {base['rays']} rays in {base['seconds']} s "
@@ -164,7 +177,7 @@ def measure_pmc(config, views, kernel, timeout_s=150):
         return None, "rocprofv3 not found", {}
     med = {}
     with tempfile.TemporaryDirectory(prefix="bench_pmc_") as tmp:
-        for group in (("FETCH_SIZE",), ("WRITE_SIZE",), SQ_PASS):
+        for group in (("FETCH_SIZE",), ("WRITE_SIZE",), SQ_PASS, L2_PASS):
             out = os.path.join(tmp, group[0])
             cmd = ["timeout", "-s", "KILL", str(timeout_s), exe, "--pmc", *group, "--kernel-trace", "--output-format",
                    "csv", "-d", out, "-o", "run", "--", sys.executable, os.path.join(REPO, "tools", "prof_target.py"),
@@ -359,7 +372,7 @@ def main():
     cst = step()
     R.set_counting(False)
     # lane use of the traversal (counting build): lane node visits / (64 x wave node steps), same for records
-    cdbg = [int(x) for x in ctx.debug_counters()[:7]]
+    cdbg = [int(x) for x in ctx.debug_counters()[:28]]
     for _ in range(args.warmup):
         step()
 
@@ -515,10 +528,42 @@ def main():
                         "algorithmic bytes (SURVEY.md 8d), most of them served by L2 / MALL (traffic = DRAM bytes)"}
         else:
             line["roofline"]["limiter"] = {"lane_use": lane_use}
+        if "TCC_HIT_sum" in pmc_med:
+            # beside the HBM fraction (SURVEY.md 8d's algorithmic bytes over the HBM peak): the rate the caches serve
+            # such gathers at, weighted by this run's L2 hit rate -- the time-weighted blend of the guide's L2 and
+            # Infinity-Cache gather rates.  The guide measured whole 1 152-B rows; the kernel gathers 16-B pieces per
+            # lane, so this is an approximate ceiling
+            hits_, miss_ = float(pmc_med["TCC_HIT_sum"]), float(pmc_med["TCC_MISS_sum"])
+            h = hits_ / max(1.0, hits_ + miss_)
+            ceil_tbs = 1.0 / (h / L2_GATHER_TBS + (1.0 - h) / IC_GATHER_TBS)
+            line["roofline"]["cache_ceiling"] = {
+                "l2_hit": h, "l2_gather_TBs": L2_GATHER_TBS, "ic_gather_TBs": IC_GATHER_TBS, "ceiling_GBs": ceil_tbs * 1e3,
+                "frac": achieved / (ceil_tbs * 1e3),
+                "source": "rocprofv3 --pmc TCC_HIT_sum / TCC_MISS_sum (median per launch, same run); rates from "
+                          "MI355X_MICROARCH.md 'Indexed rows: gather into LDS' (L2 16.8-18.8 TB/s, Infinity Cache 8.6 "
+                          "TB/s; whole-row gathers, so approximate for 16-B per-lane pieces)"}
+        # the ray mix of the counting pass (rank 0's launch): camera rays are one per pixel and sample; the kernels
+        # count cansee segments / light samples and the camera rays that hit nothing (rt_debug_counters [26], [27])
+        samples = 4 if prm.anti_aliasing else (int(prm.sample_size) if prm.multiple_rays else 1)
+        cam = F * min(pixels0, W * H) * samples
+        shad, cmiss = cdbg[26], cdbg[27]
+        crays = int(cst.rays)
+        line["config"]["ray_mix"] = {
+            "rays": crays, "camera": cam, "camera_no_hit": cmiss, "shadow_segments": shad,
+            "secondary": crays - cam - shad, "shaded_hits": int(cst.hits),
+            "ns_per_shaded_hit": avg_ms * 1e6 / max(1, int(cst.hits)),
+            "ns_per_ray": avg_ms * 1e6 / max(1, crays),
+            "note": "one launch of the step (counting pass, rank 0): camera = pixels x samples; shadow_segments = cansee "
+                    "segments and light samples; secondary = mirror / reflected / refracted rays; ns_per_shaded_hit = "
+                    "kernel time / shaded hits (a speed-up of background camera rays alone does not move it)"}
         if single is not None:
             line["single_frame"] = single
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(args.config, budget_s=args.cpu_budget, max_pixels=args.cpu_pixels or None)
+            # C1 / C2: BASELINE.md times the whole frame (C2 ~30 s over the four legs on the box's host); C3-C5 a
+            # bounded prefix of the 4 096-pixel sample (the whole sample: tools/cpu_baseline.py)
+            whole = args.config in ("C1", "C2") and not args.cpu_pixels
+            line["cpu_baseline"] = cpu_baseline(args.config, budget_s=480.0 if whole else args.cpu_budget,
+                                                max_pixels=args.cpu_pixels or None)
         print(json.dumps(line), flush=True)
     ctx.close()  # explicitly: no HIP teardown left to interpreter exit
     if ipc is not None and not ipc.owner:  # the importers unmap rank 0's images before rank 0 frees them

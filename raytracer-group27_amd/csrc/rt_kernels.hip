@@ -167,6 +167,8 @@ struct Cnt {
     // node visits that re-test a node popped from the stack (slot mask < 0xFF), the popped groups' slot
     // counts and how many of those slots still hit (counting builds: the cost of the re-visit scheme)
     uint32_t rv, rvk, rvj;
+    // the ray mix (counting builds): cansee segments and light samples, camera queries that hit nothing
+    uint32_t shad, cmiss;
 };
 
 // reference-box tests of candidate culling (ref_slab): lane evaluations, the wave's executions (the most any lane
@@ -707,6 +709,12 @@ __device__ void flush_counters(const KParams& P, const Cnt& c) {
             unsigned long long v = xs[k];
             for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
             if ((threadIdx.x & 63) == 0) atomicAdd(P.stats + RT_STATS_EXTRA + k, v);
+        }
+        const uint32_t mix[2] = {c.shad, c.cmiss};  // rt_debug_counters [26], [27]
+        for (int k = 0; k < 2; ++k) {
+            unsigned long long v = mix[k];
+            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+            if ((threadIdx.x & 63) == 0) atomicAdd(P.stats + RT_STATS_EXTRA + 10 + k, v);
         }
     }
 }

@@ -1005,10 +1005,19 @@ __device__ __attribute__((noinline)) bool advance_lane_call(const void* ka, Lane
 #define RT_V_SPLIT 128   // opaque kernel: a node's shadow segment traced beside its mirror child (split_node)
 #define RT_V_W5 512      // opaque kernel: compiled for 5 waves per SIMD (96 VGPRs; with NOCOOP its LDS fits 20 blocks)
 #define RT_V_WAVES(V) (((V) & RT_V_W5) ? 5 : ((V) & RT_V_W4) ? 4 : ((V) & RT_V_W3) ? 3 : 2)
-#define RT_V_GLDS 1024   // opaque kernel: the visitors' nodes fetched cooperatively by LDS-DMA (node_stage_glds)
-#ifndef RT_GLDS_CAP
-#define RT_GLDS_CAP 43   // GLDS: nodes one step stages in LDS (5.4 KB + the visitor list: the drain lane groups' 5 760 B)
-#endif
+
+// the ray mix of counting builds: a query starts (a cansee segment or light sample, or a camera ray: level 0, not a
+// segment) and ends (a camera ray that found nothing)
+template <bool COUNT>
+__device__ __forceinline__ void count_start(Cnt& cnt, bool shadow, uint32_t level, bool& qcam) {
+    if (!COUNT) return;
+    if (shadow) cnt.shad++;
+    qcam = !shadow && level == 0u;
+}
+template <bool COUNT>
+__device__ __forceinline__ void count_end(Cnt& cnt, bool qcam, bool found) {
+    if (COUNT && qcam && !found) cnt.cmiss++;
+}
 
 template <bool COUNT, bool TEX, int V>
 __device__ __forceinline__ bool advance_v(const KParams& P, const JobSrc& J, const void* ka, Lane& L, Frame* fr,
@@ -1076,6 +1085,9 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_kernel(KParams P
             job_rays++;
             hit = trace_query8<COUNT, 8>(S, q.o, q.d, q.t, L.sdist - 2.0f * 0.0005f, L.shadow || P.use_bvh,
                                          L.shadow && S.all_opaque, b, stk, cnt);
+            bool qcam = false;
+            count_start<COUNT>(cnt, L.shadow, L.level, qcam);
+            count_end<COUNT>(cnt, qcam, hit);
         }
         if (!busy) continue;
         if (COUNT && wave_leader()) cnt.wadv++;
@@ -1171,69 +1183,6 @@ __device__ __forceinline__ void node_fetch(const float4* nodes, uint32_t cur, fl
     const float4* np = nodes + (size_t)(cur >> 8) * 8;
 #pragma unroll
     for (int k = 0; k < 8; ++k) g[k] = np[k];
-}
-
-// ---- cooperative node fetch by LDS-DMA (RT_V_GLDS) ------------------------------------------
-// A per-lane node fetch is 8 global_load_dwordx4, every active lane on its own 128-B line: each instruction costs
-// the vector memory pipe ~17 cycles plus ~0.75 per line whatever the exec mask (tools/td_probe.hip), and the pipe
-// is what C3's launch waits on (TD busy 0.945).  Here the wave's visitors (ranked from a rotating
-// start lane) have their nodes gathered by global_load_lds_dwordx4: instruction k has lane i fetch 16-B chunk
-// (i & 7) ^ (v & 7) of the node of visitor v = 8k + i / 8, which the instruction writes to LDS entry 64k + i
-// (wave-uniform base + 16 B x lane) -- 8 whole lines per instruction, ceil(visitors / 8) instructions, no VGPR on
-// the way.  Visitor v reads its chunk c back from entry 8v + (c ^ (v & 7)) (the swizzle spreads a read-back group
-// over the banks).  The DMA is issued before the step's record loads, so one memory round trip serves both halves
-// of a dual step without the node's 32 registers live across the record test (the register-staged overlap
-// spilled: DESIGN.md 6e).  The root, where every query starts, is read from its own LDS copy and takes no slot.
-// Visitors past the stage's RT_GLDS_CAP slots visit in a later step (the rotating start keeps that fair); a lane's
-// own sequence of records and node visits is unchanged, and the same node bits reach the same box tests, so the
-// walk and every result are bit-identical.
-typedef float rt_v4f __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) rt_v4f rt_lds_f4;
-typedef __attribute__((address_space(3))) int rt_lds_i32;
-typedef __attribute__((address_space(3))) void* rt_lds_ptr;
-typedef __attribute__((address_space(1))) void* rt_gbl_ptr;
-
-// rank: the lane's place among the visitors (a visitor with rank >= RT_GLDS_CAP waits); returns the staged count
-template <int CAP>
-__device__ __forceinline__ int node_stage_glds(const float4* nodes, rt_lds_f4* stage, rt_lds_i32* sidx, bool visit,
-                                               uint32_t node, int lane, int rot, int& rank) {
-    const unsigned long long vm = __ballot(visit);
-    const int total = __popcll(vm);
-    const int below = __popcll(vm & ((1ull << lane) - 1ull)), before_rot = __popcll(vm & ((1ull << rot) - 1ull));
-    rank = lane >= rot ? below - before_rot : total - before_rot + below;
-    const int n = total < CAP ? total : CAP;
-    if (visit && rank < CAP) sidx[rank] = (int)node;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    const int v0 = lane >> 3;
-    constexpr int NG = (CAP + 7) / 8;
-    int idx[NG];
-#pragma unroll
-    for (int k = 0; k < NG; ++k) idx[k] = sidx[8 * k + v0 < CAP ? 8 * k + v0 : CAP - 1];
-#pragma unroll
-    for (int k = 0; k < NG; ++k) {
-        if (8 * k >= n) break;
-        const int v = 8 * k + v0;
-        if (v < n) {
-            const int c = (lane & 7) ^ (v & 7);
-            __builtin_amdgcn_global_load_lds((rt_gbl_ptr)(nodes + (size_t)(uint32_t)idx[k] * 8 + c),
-                                             (rt_lds_ptr)(stage + 64 * k), 16, 0, 0);
-        }
-    }
-    return n;
-}
-
-// the staged node of visitor `rank` (its DMA waited for), or the root's copy
-__device__ __forceinline__ void node_from_stage(const rt_lds_f4* stage, const rt_lds_f4* root, bool is_root, int rank,
-                                                float4 (&g)[8]) {
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the stage's DMA has landed
-    const rt_lds_f4* p = is_root ? root : stage + 8 * rank;
-    const int sw = is_root ? 0 : (rank & 7);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const rt_v4f e = p[k ^ sw];
-        g[k] = make_float4(e.x, e.y, e.z, e.w);
-    }
 }
 
 // One node visit (node in g): box tests of its slots, the next node (whose 128 B are requested
@@ -1916,6 +1865,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
     uint32_t job_rays = 0;                       // queries of the lane's current job (rt_shade ray counts)
     int xr = (int)(blockIdx.x & 7), xtried = 0;  // J.xq: the job range this wave draws from, ranges used up
     bool tracing = false;                        // a query is in flight
+    bool qcam = false;                           // counting builds: the query in flight is a camera ray
     bool pending = false;                        // a finished query waits for advance_lane
     const int refill_at = kernel_params(ka).refill;
     // wave trace of the drain (after this wave first found the job queue empty)
@@ -2114,6 +2064,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
         if (COUNT) cnt.cyc_d += (unsigned long long)clock64() - tJ;  // job fetch and camera rays
         if (start) {
             cnt.rays++;
+            count_start<COUNT>(cnt, qshadow, L.level, qcam);
             if (ray_fan < 0) job_rays++;  // a fan sample counts for its owner's job (ft.traced)
             trav_init_q(S, P.use_bvh != 0, q.o, q.d, q.t, qshadow, qsdist, T);
             tracing = true;
@@ -2151,6 +2102,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
             }
             if (tracing && !leaf_pending(T) && T.cur == RT_TRAV_NONE) {
                 trav_finish(S, T);
+                count_end<COUNT>(cnt, qcam, T.found);
                 tracing = false;
                 pending = true;
             }
@@ -2200,6 +2152,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
             if (tracing) {
                 coop_get(T, coop_q, r);
                 trav_finish(S, T);
+                count_end<COUNT>(cnt, qcam, T.found);
                 tracing = false;
                 pending = true;
             }
@@ -2538,25 +2491,13 @@ __device__ __forceinline__ v3 split_fold(const KParams& P, const SplitLane& L, i
 template <bool COUNT, int V>
 __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KParams, JobSrc) {
     constexpr bool PF = !(V & RT_V_NOPF), COOP = !(V & RT_V_NOCOOP), DIRECT = !(V & RT_V_REVISIT);
-    constexpr bool SPLIT = (V & RT_V_SPLIT) != 0, GLDS = (V & RT_V_GLDS) != 0;
-    static_assert(!(GLDS && PF), "the LDS-DMA node stage replaces the register prefetch");
+    constexpr bool SPLIT = (V & RT_V_SPLIT) != 0;
     // the kernel's arguments are read where each phase uses them (fresh_kernarg), not held in SGPRs
     const void* ka = (const void*)__builtin_amdgcn_kernarg_segment_ptr();
 #define RT_FRESH const KParams& P = *(const KParams*)fresh_kernarg(ka); const DevScene& S = P.S
     __shared__ int stack_lds[RT_STACK8 * RT_WAVE];
-    // drain lane groups (COOP): node groups of the wave's last queries, then those queries; GLDS: the same memory
-    // holds the traversal steps' node stage and visitor list (the lane groups run after the traversal loop)
-    constexpr int COOP_WORDS = COOP ? COOP_POOL + CQ_N * COOP_Q : 1;
-    // (the 4-wave build stages RT_GLDS_CAP nodes in the lane groups' memory; the 3-wave build, with LDS for 12 blocks
-    // per CU, stages every lane's)
-    constexpr int GCAP = (V & RT_V_W3) ? RT_WAVE : RT_GLDS_CAP;
-    constexpr int GLDS_WORDS = GLDS ? GCAP * 32 + RT_WAVE : 1;
-    __shared__ __attribute__((aligned(16))) int coop_mem[COOP_WORDS > GLDS_WORDS ? COOP_WORDS : GLDS_WORDS];
-    int* const coop_pool = coop_mem;
-    int* const coop_q = coop_mem + (COOP ? COOP_POOL : 0);
-    rt_lds_f4* const stage = (rt_lds_f4*)coop_mem;
-    rt_lds_i32* const sidx = (rt_lds_i32*)coop_mem + GCAP * 32;
-    __shared__ float4 root_lds[GLDS ? 8 : 1];  // GLDS: the BVH8 root (every query's first node)
+    __shared__ int coop_pool[COOP ? COOP_POOL : 1];   // drain lane groups (COOP): node groups of the wave's last queries
+    __shared__ int coop_q[COOP ? CQ_N * COOP_Q : 1];  // ... and those queries
     __shared__ int s_base, s_lim;
     __shared__ RefLds ref_lds;             // the reference BVH's boxes and leaf paths (candidate culling)
     __shared__ uint32_t split_res[SPLIT ? RT_WAVE : 1];  // SPLIT: per owner lane, segments done | visible << 16
@@ -2564,12 +2505,10 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
     int* stk = stack_lds + lane_id;
     if (RT_REF_LDS) {
         ref_lds_load(kernel_params(ka).S, ref_lds, lane_id);
-        if (GLDS && lane_id < 8 && kernel_params(ka).S.ntri > 0) root_lds[lane_id] = kernel_params(ka).S.nodes[lane_id];
         __syncthreads();
     }
     const unsigned long long t_wave0 = (COUNT && kernel_params(ka).wave_trace) ? wall_clock64() : 0ull;
     unsigned int wave_jobs = 0;
-    int grot = 0;  // GLDS: the visitors' rotating start lane
     std::conditional_t<SPLIT, SplitLane, LiteLane> L;
     L.job = -1;
     if constexpr (SPLIT) {
@@ -2584,6 +2523,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
     SlabCnt slab{};
     int xr = (int)(blockIdx.x & 7), xtried = 0;
     bool tracing = false, pending = false;
+    bool qcam = false;  // counting builds: the query in flight is a camera ray
     unsigned long long t_exh = 0ull;
     unsigned int it_drain = 0, lanes_drain = 0, coop_n = 0, pa_drain = 0;  // wave trace, counting builds only
     uint32_t qn0 = 0, qr0 = 0;  // counting builds: the lane's node / record counts when its query started
@@ -2745,6 +2685,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
             Trav Tn;
             if (start) {
                 cnt.rays++;
+                count_start<COUNT>(cnt, qshadow, L.level, qcam);
                 trav_init_q(S, P.use_bvh != 0, q.o, q.d, q.t, qshadow, qsdist, Tn);
                 tracing = true;
                 // counting builds: queries whose direction is not unit walk every record (debug counter 28)
@@ -2790,19 +2731,6 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
                 const int ntr = __popcll(__ballot(tracing));
                 if (wave_leader()) cnt.hist[min((ntr - 1) >> 4, 2)]++;
             }
-            // GLDS: the nodes this step visits, staged before the record loads (a lane visits when it has no leaf
-            // work, or in a dual step when its record step takes the last record: the record cursor's pop of lh;
-            // an any-hit record ending the query leaves its staged node unused)
-            int grank = 0;
-            bool groot = false;
-            if constexpr (GLDS) {
-                const bool gv = tracing && T.cur != RT_TRAV_NONE &&
-                                (!leaf_pending(T) || (P.dual && (T.rk > 0 ? T.lh == 0u : (T.lh & (T.lh - 1u)) == 0u)));
-                groot = (T.cur >> 8) == 0u;
-                node_stage_glds<GCAP>(S.nodes, stage, sidx, gv && !groot, T.cur >> 8, lane_id, grot, grank);
-                if (groot) grank = 0;
-                grot = (grot + 23) & 63;
-            }
             if (tracing) {
                 const bool rec = leaf_pending(T);
                 if (rec) trav_record<COUNT, true, false, true>(S, T, cnt, nullptr, COUNT ? &slab : nullptr, &ref_lds);
@@ -2812,24 +2740,17 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
                     for (uint32_t k = 0; k < 8u; ++k) w += __ballot(ns > k) ? 1u : 0u;
                     if (wave_leader()) slab.wslab += w;
                 }
-                // (GLDS: a visitor past the stage's slots visits in a later step)
-                const bool nv = T.cur != RT_TRAV_NONE && (!rec || (P.dual && T.lh == 0u)) && (!GLDS || grank < GCAP);
+                const bool nv = T.cur != RT_TRAV_NONE && (!rec || (P.dual && T.lh == 0u));
                 if (COUNT) {
                     slab.iters++;
                     if (nv && rec) slab.both++;
                     if (!nv && T.cur != RT_TRAV_NONE) slab.blocked++;
                 }
-                if constexpr (GLDS) {
-                    if (nv) {
-                        node_from_stage(stage, (const rt_lds_f4*)root_lds, groot, grank, g);
-                        trav_node<COUNT, 8, false, DIRECT, false, true>(S, T, stk, g, cnt);
-                    }
-                } else {
-                    if (nv) trav_node<COUNT, 8, PF, DIRECT>(S, T, stk, g, cnt);
-                }
+                if (nv) trav_node<COUNT, 8, PF, DIRECT>(S, T, stk, g, cnt);
             }
             if (tracing && !leaf_pending(T) && T.cur == RT_TRAV_NONE) {
                 trav_finish(S, T);
+                count_end<COUNT>(cnt, qcam, T.found);
                 tracing = false;
                 pending = true;
                 // counting builds: the longest queries (debug counters 29 / 30: most node visits / records of one
@@ -2899,6 +2820,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
             if (tracing) {
                 coop_get(T, coop_q, r);
                 trav_finish(S, T);
+                count_end<COUNT>(cnt, qcam, T.found);
                 tracing = false;
                 pending = true;
             }
@@ -3243,6 +3165,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_tree_kernel(KPar
     Cnt cnt{};
     int xr = (int)(blockIdx.x & 7), xtried = 0;
     bool tracing = false, pending = false;
+    bool qcam = false;  // counting builds: the query in flight is a camera ray
     for (;;) {
         unsigned long long tA = COUNT ? (unsigned long long)clock64() : 0ull;
         RT_FRESH;
@@ -3435,6 +3358,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_tree_kernel(KPar
             Trav Tn;
             if (start) {
                 cnt.rays++;
+                count_start<COUNT>(cnt, qshadow, L.level, qcam);
                 trav_init_q(S, P.use_bvh != 0, q.o, q.d, q.t, qshadow, qsdist, Tn);
                 tracing = true;
             } else {
@@ -3468,6 +3392,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_tree_kernel(KPar
             }
             if (tracing && !leaf_pending(T) && T.cur == RT_TRAV_NONE) {
                 trav_finish(S, T);
+                count_end<COUNT>(cnt, qcam, T.found);
                 tracing = false;
                 pending = true;
             }

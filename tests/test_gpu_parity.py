@@ -285,7 +285,6 @@ def test_kernel_variants_bit_identical(R, ctxs, golden_dir, case):
                                               ("C3", (200, 80), "", 0), ("C3", (200, 80), "tail", 0),
                                               ("C3", (200, 80), "wf", 0), ("C2", None, "wf", 0),
                                               ("C3", (200, 80), "split", 0), ("C3", (200, 80), "split", 1),
-                                              ("C3", (200, 80), "glds", 0), ("C3", (200, 80), "glds", 1),
                                               ("C4", (200, 80), "", 0), ("C5", None, "", 0)])
 def test_view_batch_bit_identical(R, O, ctxs, cfg, uv, kernel, aa):
     """rt_render_views_device: every view of a batch is bit-identical to rt_render_device with that
@@ -301,8 +300,6 @@ def test_view_batch_bit_identical(R, O, ctxs, cfg, uv, kernel, aa):
         opts = {R.OPT_KERNEL: R.KERNEL_DYNAMIC_FETCH, R.OPT_WAVEFRONT: 1}
     if kernel == "split":  # the opaque kernel with the shadow segments traced beside the mirror chain
         opts = {R.OPT_KERNEL: R.KERNEL_DYNAMIC_FETCH, R.OPT_OPAQUE: 4}
-    if kernel == "glds":  # ... with the visitors' nodes staged by LDS-DMA
-        opts = {R.OPT_KERNEL: R.KERNEL_DYNAMIC_FETCH, R.OPT_OPAQUE: 8}
     with V.options(R, ctx, opts):
         _view_batch_checks(R, O, scene, ctx, prm, cfg, aa)
 
@@ -481,7 +478,7 @@ def test_split_depths_and_samples(R, O, depth, multi):
         cam = R.camera_from_trackball(aspect=R.aspect_of(W, H))
         ref, rays = O.Oracle(scene).render(prm, W, H)
         base = None
-        for opaque in (1, 4, 5, 8):
+        for opaque in (1, 4, 5):
             with V.options(R, ctx, {R.OPT_KERNEL: R.KERNEL_DYNAMIC_FETCH, R.OPT_OPAQUE: opaque}):
                 img, st = ctx.render(cam, prm, W, H)
             assert st.rays == rays, opaque
@@ -508,7 +505,7 @@ def test_split_single_spot_light(R, O):
         cam = R.camera_from_trackball(aspect=R.aspect_of(W, H))
         ref, rays = O.Oracle(scene).render(prm, W, H)
         base = None
-        for opaque in (0, 1, 4, 5, 7, 8):
+        for opaque in (0, 1, 4, 5, 7):
             with V.options(R, ctx, {R.OPT_KERNEL: R.KERNEL_DYNAMIC_FETCH, R.OPT_OPAQUE: opaque}):
                 img, st = ctx.render(cam, prm, W, H)
             assert st.rays == rays, opaque

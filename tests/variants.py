@@ -40,7 +40,6 @@ def all_variants(R):
         {R.OPT_KERNEL: df, R.OPT_OPAQUE: 4},                    # ... its 4-wave build, segments beside the mirror chain
         {R.OPT_KERNEL: df, R.OPT_OPAQUE: 5},                    # ... the same in the 3-wave build
         {R.OPT_KERNEL: df, R.OPT_OPAQUE: 7},                    # ... SPLIT without the drain lane groups
-        {R.OPT_KERNEL: df, R.OPT_OPAQUE: 8},                    # ... nodes staged by LDS-DMA (GLDS)
         {R.OPT_KERNEL: df, R.OPT_PRIO: 4},                      # ... issue priority after 4 iterations of a phase
         {R.OPT_KERNEL: df, R.OPT_REFILL: 32},                   # ... and a half-wave refill
         {R.OPT_KERNEL: df, R.OPT_COOP: 1},                      # ... drain lane groups in the drain only
