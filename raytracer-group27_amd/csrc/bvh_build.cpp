@@ -812,11 +812,11 @@ Bvh8 build_bvh8(const Bvh2& b2, int width) {
     struct Done {
         Child2 ch[8];
         int nch = 0, n_inner = 0, n_rec = 0;
-        uint32_t w[32];
+        uint32_t w[RT_NODE_SDW];
     };
     const int nth = host_threads();
     std::vector<Item> level{{0, 0, 1}};
-    out.nodes.assign(32, 0u);
+    out.nodes.assign(RT_NODE_SDW, 0u);
     while (!level.empty()) {
         const int m = (int)level.size();
         std::vector<Done> done(m);
@@ -857,14 +857,14 @@ Bvh8 build_bvh8(const Bvh2& b2, int width) {
                 for (int a = 0; a < 3; ++a) {
                     std::memcpy(&w[a], &lo[a], 4);
                     const double ext = (double)hi[a] - (double)lo[a];
-                    // the smallest ex >= -126 with 65000 * 2^ex >= ext (frexp's guess, then the exact test)
+                    // the smallest ex >= -126 with RT_PLANE_STEPS * 2^ex >= ext (frexp's guess, then the exact test)
                     int ex = -126;
                     if (ext > 0.0) {
                         int fe = 0;
-                        std::frexp(ext / 65000.0, &fe);
+                        std::frexp(ext / RT_PLANE_STEPS, &fe);
                         ex = std::max(-126, fe - 2);
                     }
-                    while (ex < 127 && std::ldexp(65000.0, ex) < ext) ++ex;
+                    while (ex < 127 && std::ldexp(RT_PLANE_STEPS, ex) < ext) ++ex;
                     // the device forms 2^e * (1/d) with |1/d| <= 1e20: keep it finite
                     if (ex > 40) err[j] = "BVH8: scene extent too large to quantise";
                     e[a] = ex;
@@ -872,7 +872,7 @@ Bvh8 build_bvh8(const Bvh2& b2, int width) {
                 w[3] = (uint32_t)(e[0] + 127) | ((uint32_t)(e[1] + 127) << 8) | ((uint32_t)(e[2] + 127) << 16) |
                        ((uint32_t)axis << 24);
                 uint32_t imask = 0, lmask = 0, counts = 0;
-                uint16_t q[6][8];
+                uint32_t q[6][8];
                 for (int sl = 0; sl < 8; ++sl)
                     for (int k = 0; k < 6; ++k) q[k][sl] = (k < 3) ? plane_max() : 0;  // empty: inverted box
                 for (size_t sl = 0; sl < ch.size(); ++sl) {
@@ -886,8 +886,8 @@ Bvh8 build_bvh8(const Bvh2& b2, int width) {
                         while (qh < qmax && decode(lo[a], e[a], (uint32_t)qh) < c.hi[a]) ++qh;
                         if (decode(lo[a], e[a], (uint32_t)ql) > c.lo[a] || decode(lo[a], e[a], (uint32_t)qh) < c.hi[a])
                             err[j] = "BVH8 quantisation is not conservative";
-                        q[a][sl] = (uint16_t)ql;
-                        q[3 + a][sl] = (uint16_t)qh;
+                        q[a][sl] = (uint32_t)ql;
+                        q[3 + a][sl] = (uint32_t)qh;
                     }
                     if (c.count > 0) {
                         lmask |= 1u << sl;
@@ -902,31 +902,29 @@ Bvh8 build_bvh8(const Bvh2& b2, int width) {
                 D.nch = (int)ch.size();
                 w[6] = imask | (lmask << 8);
                 w[7] = counts;
-                for (int k = 0; k < 6; ++k)
-                    for (int sl = 0; sl < 8; sl += 2)
-                        w[8 + k * 4 + sl / 2] = (uint32_t)q[k][sl] | ((uint32_t)q[k][sl + 1] << 16);
+                pack_planes(w, q);
             }
         });
         for (const std::string& e : err)
             if (!e.empty()) throw std::runtime_error(e);
         // number the children and records in level order
         std::vector<int> child_base(m), tri_base(m);
-        int nodes_total = (int)(out.nodes.size() / 32), rec_total = (int)out.order.size();
+        int nodes_total = (int)(out.nodes.size() / RT_NODE_SDW), rec_total = (int)out.order.size();
         for (int j = 0; j < m; ++j) {
             child_base[j] = nodes_total;
             tri_base[j] = rec_total;
             nodes_total += done[j].n_inner;
             rec_total += done[j].n_rec;
         }
-        out.nodes.resize((size_t)nodes_total * 32, 0u);
+        out.nodes.resize((size_t)nodes_total * RT_NODE_SDW, 0u);
         out.order.resize(rec_total);
         std::vector<Item> next;
-        next.reserve(nodes_total - (int)(out.nodes.size() / 32) + m * 8);
+        next.reserve(nodes_total - (int)(out.nodes.size() / RT_NODE_SDW) + m * 8);
         for (int j = 0; j < m; ++j) {
             Done& D = done[j];
             D.w[4] = (uint32_t)child_base[j];
             D.w[5] = (uint32_t)tri_base[j];
-            std::memcpy(out.nodes.data() + (size_t)level[j].slot * 32, D.w, sizeof(D.w));
+            std::memcpy(out.nodes.data() + (size_t)level[j].slot * RT_NODE_SDW, D.w, sizeof(D.w));
             out.max_depth = std::max(out.max_depth, level[j].depth);
             int rank = 0, r = tri_base[j];
             for (int sl = 0; sl < D.nch; ++sl) {

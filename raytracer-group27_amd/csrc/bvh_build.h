@@ -69,16 +69,17 @@ Bvh2 build_bvh2(const float* positions, int ntri, float eps, int max_leaf = RT_M
 
 // Wide BVH collapsed from a Bvh2 (greedy: open the child with the largest area until `width`
 // children, width <= 8; slots past `width` stay empty),
-// 128-B nodes with 16-bit child boxes quantised conservatively against the node origin:
+// 128-B nodes with 16-bit child boxes (80-B nodes with 8-bit ones: RT_PLANES_U8, pack_planes) quantised
+// conservatively against the node origin:
 //   dword 0-2 origin xyz (f32) | 3: (ex+127) | (ey+127)<<8 | (ez+127)<<16 (scale = 2^e)
 //   4: child_base (first internal child node; internal children are contiguous in slot order)
 //   5: tri_base (first record of the node's leaf children, contiguous in slot order)
 //   6: internal-child mask | leaf-child mask << 8
 //   7: per-slot triangle count, 4 bits per slot (0 for internal / empty slots)
-//   8-31: q_lo_x[8] q_lo_y[8] q_lo_z[8] q_hi_x[8] q_hi_y[8] q_hi_z[8] as uint16
+//   8-31: q_lo_x[8] q_lo_y[8] q_lo_z[8] q_hi_x[8] q_hi_y[8] q_hi_z[8] as uint16 (RT_PLANES_U8: 8-19, as uint8)
 // decoded bound = origin + float(q) * 2^e, verified on the host to contain the child box.
 struct Bvh8 {
-    std::vector<uint32_t> nodes;  // 32 dwords per node
+    std::vector<uint32_t> nodes;  // RT_NODE_DW dwords per node
     std::vector<int> order;       // record i -> scene triangle index
     int max_depth = 0;
 };
@@ -88,19 +89,46 @@ Bvh8 build_bvh8(const Bvh2& b2, int width = 8);
 // f(begin, end) over [0, n) in chunks of `chunk`, on the host's threads (scene upload loops)
 void parallel_chunks(int n, int chunk, const std::function<void(int, int)>& f);
 
-#ifndef RT_PLANES_F16
-#define RT_PLANES_F16 1  // BVH8 child planes: IEEE half offsets (1) or 16-bit integers (0; until round 4)
+#ifndef RT_PLANES_U8
+#define RT_PLANES_U8 0  // BVH8 child planes: 8-bit integer steps in 80-B nodes (1) or 16-bit words in 128-B nodes (0)
 #endif
+#ifndef RT_PLANES_F16
+#define RT_PLANES_F16 1  // 16-bit planes: IEEE half offsets (1) or 16-bit integers (0; until round 4)
+#endif
+// dwords per BVH8 node: the 8-dword header, then the six planes of the 8 slots (1 or 2 bytes each)
+#define RT_NODE_DW (RT_PLANES_U8 ? 20 : 32)
+#define RT_NODE_F4 (RT_NODE_DW / 4)
+// the node stride in dwords: RT_NODE_PAD keeps 80-B nodes on 128-B lines (5 loads, one line per node)
+#ifndef RT_NODE_PAD
+#define RT_NODE_PAD 0
+#endif
+#define RT_NODE_SDW ((RT_PLANES_U8 && RT_NODE_PAD) ? 32 : RT_NODE_DW)
+#define RT_NODE_SF4 (RT_NODE_SDW / 4)
+// the exponent rule's step budget: the smallest e with RT_PLANE_STEPS * 2^e >= the node's extent on the axis
+#define RT_PLANE_STEPS (RT_PLANES_U8 ? 255.0 : 65000.0)
 
-// BVH8 child planes (both builders, every traversal): a plane of axis a is origin[a] + q * 2^e[a] with q a 16-bit
-// word -- an IEEE binary16 value (RT_PLANES_F16: the traversal's slab distance is one v_fma_mix_f32 per plane,
-// the half widened inside the fma) or an unsigned integer.  plane_q is q's value; plane_max the largest word.
+// BVH8 child planes (both builders, every traversal): a plane of axis a is origin[a] + q * 2^e[a] with q an 8-bit
+// integer (RT_PLANES_U8), or a 16-bit word -- an IEEE binary16 value (RT_PLANES_F16: the traversal's slab distance is
+// one v_fma_mix_f32 per plane, the half widened inside the fma) or an unsigned integer.  plane_q is q's value;
+// plane_max the largest word.
 RT_HD float plane_q(uint32_t q) {
-    if (!RT_PLANES_F16) return (float)q;
+    if (RT_PLANES_U8 || !RT_PLANES_F16) return (float)q;
     const uint32_t m = q & 0x3FFu, ex = (q >> 10) & 0x1Fu;  // non-negative finite halves only (q <= 0x7BFF)
     return ex == 0 ? (float)m * 5.9604644775390625e-08f : ldexpf(1.0f + (float)m * 0.0009765625f, (int)ex - 15);
 }
-RT_HD uint32_t plane_max() { return RT_PLANES_F16 ? 0x7BFFu : 65535u; }
+RT_HD uint32_t plane_max() { return RT_PLANES_U8 ? 255u : RT_PLANES_F16 ? 0x7BFFu : 65535u; }
+// the plane words into node dwords 8.. : plane k (lo x, y, z, hi x, y, z) of slot sl at byte sl of the plane's
+// 8 bytes (U8: dwords 8 + 2k, 9 + 2k) or at half-word sl of its 16 bytes (dwords 8 + 4k .. 11 + 4k)
+RT_HD void pack_planes(uint32_t* w, const uint32_t (&q)[6][8]) {
+    for (int k = 0; k < 6; ++k) {
+        if (RT_PLANES_U8) {
+            for (int h = 0; h < 2; ++h)
+                w[8 + 2 * k + h] = q[k][4 * h] | (q[k][4 * h + 1] << 8) | (q[k][4 * h + 2] << 16) | (q[k][4 * h + 3] << 24);
+        } else {
+            for (int sl = 0; sl < 8; sl += 2) w[8 + k * 4 + sl / 2] = q[k][sl] | (q[k][sl + 1] << 16);
+        }
+    }
+}
 // the largest word whose value is <= x (x >= 0), and the smallest whose value is >= x: the conservative rounding
 // of a child's lo / hi plane (values grow with the word, so a binary search over the words)
 RT_HD uint32_t plane_down(double x) {

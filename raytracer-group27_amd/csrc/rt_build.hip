@@ -946,9 +946,9 @@ __global__ void k_collapse(const Item8* __restrict__ items, int m, const Bvh2Nod
         --nch;
         for (int i = 0; i < ns; ++i) ch[nch++] = sub[i];
     }
-    uint32_t* w = words + (size_t)j * 32;
-    uint32_t wl[32];
-    for (int k = 0; k < 32; ++k) wl[k] = 0u;
+    uint32_t* w = words + (size_t)j * RT_NODE_SDW;
+    uint32_t wl[RT_NODE_SDW];
+    for (int k = 0; k < RT_NODE_SDW; ++k) wl[k] = 0u;
     float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
     for (int i = 0; i < nch; ++i)
         for (int a = 0; a < 3; ++a) {
@@ -963,10 +963,10 @@ __global__ void k_collapse(const Item8* __restrict__ items, int m, const Bvh2Nod
         int ex = -126;
         if (ext > 0.0) {
             int fe = 0;
-            frexp(ext / 65000.0, &fe);
+            frexp(ext / RT_PLANE_STEPS, &fe);
             ex = max(-126, fe - 2);
         }
-        while (ex < 127 && ldexp(65000.0, ex) < ext) ++ex;
+        while (ex < 127 && ldexp(RT_PLANE_STEPS, ex) < ext) ++ex;
         if (ex > 40) atomicOr(err, 4);
         e[a] = ex;
     }
@@ -1003,9 +1003,8 @@ __global__ void k_collapse(const Item8* __restrict__ items, int m, const Bvh2Nod
     }
     wl[6] = imask | (lmask << 8);
     wl[7] = cnts;
-    for (int k = 0; k < 6; ++k)
-        for (int sl = 0; sl < 8; sl += 2) wl[8 + k * 4 + sl / 2] = q[k][sl] | (q[k][sl + 1] << 16);
-    for (int k = 0; k < 32; ++k) w[k] = wl[k];
+    pack_planes(wl, q);
+    for (int k = 0; k < RT_NODE_SDW; ++k) w[k] = wl[k];
     counts[j] = ((unsigned long long)n_inner << 32) | (unsigned)n_rec;
 }
 
@@ -1020,9 +1019,9 @@ __global__ void k_emit(const Item8* __restrict__ items, int m, const uint32_t* _
     const Item8 it = items[j];
     const int child_base = nodes_total + (int)(scan[j] >> 32);
     const int tri_base = rec_total + (int)(scan[j] & 0xFFFFFFFFull);
-    const uint32_t* w = words + (size_t)j * 32;
-    uint32_t* o = nodes8 + (size_t)it.slot * 32;
-    for (int k = 0; k < 32; ++k) o[k] = w[k];
+    const uint32_t* w = words + (size_t)j * RT_NODE_SDW;
+    uint32_t* o = nodes8 + (size_t)it.slot * RT_NODE_SDW;
+    for (int k = 0; k < RT_NODE_SDW; ++k) o[k] = w[k];
     o[4] = (uint32_t)child_base;
     o[5] = (uint32_t)tri_base;
     const uint32_t masks = w[6];
@@ -1417,10 +1416,10 @@ bool gpu_build(const float* h_pos, int ntri, const float* sph4, int nsph, GpuBui
     out.ms[1] = ms_now();  // + BVH2
     // ---- 3. BVH8 collapse, breadth first ----
     const int cap8 = hc.nodes + 1;
-    uint32_t* nodes8 = B.get<uint32_t>((size_t)cap8 * 32);
+    uint32_t* nodes8 = B.get<uint32_t>((size_t)cap8 * RT_NODE_SDW);
     int* order8 = B.get<int>(ntri);
     Item8 *items = B.get<Item8>(cap8), *items_next = B.get<Item8>(cap8);
-    uint32_t* words = B.get<uint32_t>((size_t)cap8 * 32);
+    uint32_t* words = B.get<uint32_t>((size_t)cap8 * RT_NODE_SDW);
     Child2* chl = B.get<Child2>((size_t)cap8 * 8);
     unsigned long long *cnt = B.get<unsigned long long>(cap8), *scan = B.get<unsigned long long>(cap8);
     int* d_err = B.get<int>(1);
@@ -1480,13 +1479,13 @@ bool gpu_build(const float* h_pos, int ntri, const float* sph4, int nsph, GpuBui
     float4* rec = nullptr;
     float4* n8 = nullptr;
     GB_CHECK(hipMalloc(&rec, (size_t)ntri * 64));
-    if (hipMalloc(&n8, (size_t)nodes_total * 128) != hipSuccess) {
+    if (hipMalloc(&n8, (size_t)nodes_total * RT_NODE_SDW * 4) != hipSuccess) {
         hipFree(rec);
         err = "GPU build: out of device memory";
         return false;
     }
     k_records<<<grid(ntri, 256), 256, 0, st>>>(order8, ntri, pos, tri_key, tri_leaf, rec);
-    hipError_t e = hipMemcpyAsync(n8, nodes8, (size_t)nodes_total * 128, hipMemcpyDeviceToDevice, st);
+    hipError_t e = hipMemcpyAsync(n8, nodes8, (size_t)nodes_total * RT_NODE_SDW * 4, hipMemcpyDeviceToDevice, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e == hipSuccess) e = hipGetLastError();
     if (e != hipSuccess) {

@@ -159,6 +159,21 @@ __device__ __forceinline__ float plane_f(uint32_t w, int sh) {
     else return (float)h;
 }
 
+// the value of plane k (0-5: lo x, y, z, hi x, y, z) of slot s of a node held in its float4s g (bvh_build.h
+// pack_planes): RT_PLANES_U8 an 8-bit step count (one v_cvt_f32_ubyteN of its dword), else the 16-bit word
+__device__ __forceinline__ float node_plane(const float4* g, int k, int s) {
+    if constexpr (RT_PLANES_U8) {
+        const int dw = 2 * k + (s >> 2);
+        const float4 v = g[2 + (dw >> 2)];
+        const uint32_t w = __float_as_uint((dw & 3) == 0 ? v.x : (dw & 3) == 1 ? v.y : (dw & 3) == 2 ? v.z : v.w);
+        return (float)((w >> (8 * (s & 3))) & 0xFFu);
+    } else {
+        const float4 v = g[2 + k];
+        const int wi = s >> 1;
+        return plane_f(__float_as_uint(wi == 0 ? v.x : wi == 1 ? v.y : wi == 2 ? v.z : v.w), (s & 1) * 16);
+    }
+}
+
 template <bool COUNT, int NW>
 __device__ __forceinline__ bool trace_query8(const DevScene& S, v3 o, v3 d, float t_init, float thr, bool REF,
                                              bool ANY, Best& best, int* stk, Cnt& cnt) {
@@ -178,13 +193,17 @@ __device__ __forceinline__ bool trace_query8(const DevScene& S, v3 o, v3 d, floa
         const float4* nodes = S.nodes;
         int sp = 0;
         uint32_t cur = 0xFFu;  // node 0, every slot
-        // software pipeline: the next node's 128 B are requested before this node's leaf
+        // software pipeline: the next node's bytes are requested before this node's leaf
         // triangles are tested, so the two memory latencies overlap
-        float4 g0 = nodes[0], g1 = nodes[1], g2 = nodes[2], g3 = nodes[3];
-        float4 g4 = nodes[4], g5 = nodes[5], g6 = nodes[6], g7 = nodes[7];
+        float4 g[RT_NODE_F4];
+#pragma unroll
+        for (int k = 0; k < RT_NODE_F4; ++k) g[k] = nodes[k];
         for (;;) {
             const uint32_t node = cur >> 8;
-            const float4 f0 = g0, f1 = g1, qlx = g2, qly = g3, qlz = g4, qhx = g5, qhy = g6, qhz = g7;
+            float4 gn[RT_NODE_F4];
+#pragma unroll
+            for (int k = 0; k < RT_NODE_F4; ++k) gn[k] = g[k];
+            const float4 f0 = gn[0], f1 = gn[1];
             if (COUNT) {
                 cnt.nodes++;
                 if (wave_leader()) cnt.wnodes++;
@@ -209,14 +228,9 @@ __device__ __forceinline__ bool trace_query8(const DevScene& S, v3 o, v3 d, floa
 #pragma unroll
             for (int s = 0; s < NW; ++s) {
                 if (m & (1u << s)) {
-                    const int wi = s >> 1, sh = (s & 1) * 16;
-                    auto q = [&](const float4& f) {
-                        const uint32_t wv = __float_as_uint(wi == 0 ? f.x : wi == 1 ? f.y : wi == 2 ? f.z : f.w);
-                        return plane_f(wv, sh);
-                    };
-                    const float tlx = fmaf(q(qlx), bx, ax), thx = fmaf(q(qhx), bx, ax);
-                    const float tly = fmaf(q(qly), by, ay), thy = fmaf(q(qhy), by, ay);
-                    const float tlz = fmaf(q(qlz), bz, az), thz = fmaf(q(qhz), bz, az);
+                    const float tlx = fmaf(node_plane(gn, 0, s), bx, ax), thx = fmaf(node_plane(gn, 3, s), bx, ax);
+                    const float tly = fmaf(node_plane(gn, 1, s), by, ay), thy = fmaf(node_plane(gn, 4, s), by, ay);
+                    const float tlz = fmaf(node_plane(gn, 2, s), bz, az), thz = fmaf(node_plane(gn, 5, s), bz, az);
                     const float t0 = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fminf(tlz, thz));
                     const float t1 = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fmaxf(tlz, thz));
                     if (t0 <= t1 && t1 >= 0.0f && t0 <= tcull) {
@@ -248,9 +262,9 @@ __device__ __forceinline__ bool trace_query8(const DevScene& S, v3 o, v3 d, floa
                 more = false;
             }
             if (more) {
-                const float4* np = nodes + (size_t)(cur >> 8) * 8;
-                g0 = np[0], g1 = np[1], g2 = np[2], g3 = np[3];
-                g4 = np[4], g5 = np[5], g6 = np[6], g7 = np[7];
+                const float4* np = nodes + (size_t)(cur >> 8) * RT_NODE_SF4;
+#pragma unroll
+                for (int k = 0; k < RT_NODE_F4; ++k) g[k] = np[k];
             }
             // leaf children: records tri_base + (counts of lower leaf slots), in slot order
             uint32_t lh = hits & lmask;
@@ -1179,10 +1193,10 @@ __device__ __forceinline__ void trav_init_q(const DevScene& S, bool use_bvh, v3 
 }
 
 
-__device__ __forceinline__ void node_fetch(const float4* nodes, uint32_t cur, float4 (&g)[8]) {
-    const float4* np = nodes + (size_t)(cur >> 8) * 8;
+__device__ __forceinline__ void node_fetch(const float4* nodes, uint32_t cur, float4 (&g)[RT_NODE_F4]) {
+    const float4* np = nodes + (size_t)(cur >> 8) * RT_NODE_SF4;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) g[k] = np[k];
+    for (int k = 0; k < RT_NODE_F4; ++k) g[k] = np[k];
 }
 
 // One node visit (node in g): box tests of its slots, the next node (whose 128 B are requested
@@ -1206,7 +1220,7 @@ __device__ __forceinline__ void chk_report(unsigned long long* err, uint32_t cod
 // LOADED (the wavefront trace kernel): the caller issued the node's loads into g before its record test, so
 // both memory round trips of a dual step overlap; nothing is prefetched
 template <bool COUNT, int NW, bool PF = true, bool DIRECT = false, bool CHK = false, bool LOADED = false>
-__device__ __forceinline__ void trav_node(const DevScene& S, Trav& T, int* stk, float4 (&g)[8], Cnt& cnt,
+__device__ __forceinline__ void trav_node(const DevScene& S, Trav& T, int* stk, float4 (&g)[RT_NODE_F4], Cnt& cnt,
                                           unsigned long long* err = nullptr) {
     const uint32_t node = T.cur >> 8;
     if (CHK && node >= (uint32_t)S.nnodes) {
@@ -1217,7 +1231,7 @@ __device__ __forceinline__ void trav_node(const DevScene& S, Trav& T, int* stk, 
         return;
     }
     if (!PF && !LOADED) node_fetch(S.nodes, T.cur, g);
-    const float4 f0 = g[0], f1 = g[1], qlx = g[2], qly = g[3], qlz = g[4], qhx = g[5], qhy = g[6], qhz = g[7];
+    const float4 f0 = g[0], f1 = g[1];
     if (COUNT) {
         cnt.nodes++;
         if (wave_leader()) cnt.wnodes++;
@@ -1239,8 +1253,22 @@ __device__ __forceinline__ void trav_node(const DevScene& S, Trav& T, int* stk, 
     // value: for b > 0 the lo plane gives the smaller t, for b < 0 the hi plane, for b == 0 both are a),
     // so min/max per axis become one selection per plane word; near and far in one packed fma
     const bool sx = __float_as_uint(inv.x) >> 31, sy = __float_as_uint(inv.y) >> 31, sz = __float_as_uint(inv.z) >> 31;
-    const float4 nx = sx ? qhx : qlx, fx = sx ? qlx : qhx, ny = sy ? qhy : qly, fy = sy ? qly : qhy,
-                 nz = sz ? qhz : qlz, fz = sz ? qlz : qhz;
+    // the near and far plane words of each axis (PD dwords per plane: 8 slots of 1 or 2 bytes)
+    constexpr int PD = RT_PLANES_U8 ? 2 : 4;
+    auto dword = [&](int i) {
+        const float4 v = g[2 + (i >> 2)];
+        return __float_as_uint((i & 3) == 0 ? v.x : (i & 3) == 1 ? v.y : (i & 3) == 2 ? v.z : v.w);
+    };
+    uint32_t nw[3][PD], fw[3][PD];
+    const bool sa[3] = {sx, sy, sz};
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int j = 0; j < PD; ++j) {
+            const uint32_t lo = dword(a * PD + j), hi = dword((3 + a) * PD + j);
+            nw[a][j] = sa[a] ? hi : lo;
+            fw[a][j] = sa[a] ? lo : hi;
+        }
     typedef float f2 __attribute__((ext_vector_type(2)));
     const f2 b2x = {bx, bx}, b2y = {by, by}, b2z = {bz, bz}, a2x = {ax, ax}, a2y = {ay, ay}, a2z = {az, az};
     uint32_t hits = 0u, kbest = 0xFFFFFFFFu;
@@ -1248,17 +1276,21 @@ __device__ __forceinline__ void trav_node(const DevScene& S, Trav& T, int* stk, 
     const uint32_t ni = __popc(imask);  // DIRECT: the inner children are slots 0 .. ni - 1 (slot_order)
 #pragma unroll
     for (int s = 0; s < NW; ++s) {
-        const int wi = s >> 1, sh = (s & 1) * 16;
-        auto w = [&](const float4& v) { return __float_as_uint(wi == 0 ? v.x : wi == 1 ? v.y : wi == 2 ? v.z : v.w); };
+        // slot s's value in a plane's words: byte s & 3 of word s >> 2 (U8, one v_cvt_f32_ubyteN), else the half
+        // word s & 1 of word s >> 1
+        auto pv = [&](const uint32_t* w) {
+            if constexpr (RT_PLANES_U8) return (float)((w[s >> 2] >> (8 * (s & 3))) & 0xFFu);
+            else return plane_f(w[s >> 1], (s & 1) * 16);
+        };
         f2 tx, ty, tz;  // (near, far)
-        if constexpr (RT_PLANES_F16) {  // one v_fma_mix_f32 per plane (the half widened inside the fma)
-            tx = f2{fmaf(plane_f(w(nx), sh), bx, ax), fmaf(plane_f(w(fx), sh), bx, ax)};
-            ty = f2{fmaf(plane_f(w(ny), sh), by, ay), fmaf(plane_f(w(fy), sh), by, ay)};
-            tz = f2{fmaf(plane_f(w(nz), sh), bz, az), fmaf(plane_f(w(fz), sh), bz, az)};
+        if constexpr (RT_PLANES_F16 && !RT_PLANES_U8) {  // one v_fma_mix_f32 per plane (the half widened inside the fma)
+            tx = f2{fmaf(pv(nw[0]), bx, ax), fmaf(pv(fw[0]), bx, ax)};
+            ty = f2{fmaf(pv(nw[1]), by, ay), fmaf(pv(fw[1]), by, ay)};
+            tz = f2{fmaf(pv(nw[2]), bz, az), fmaf(pv(fw[2]), bz, az)};
         } else {  // integer planes: converted, then near and far in one packed fma
-            tx = __builtin_elementwise_fma(f2{plane_f(w(nx), sh), plane_f(w(fx), sh)}, b2x, a2x);
-            ty = __builtin_elementwise_fma(f2{plane_f(w(ny), sh), plane_f(w(fy), sh)}, b2y, a2y);
-            tz = __builtin_elementwise_fma(f2{plane_f(w(nz), sh), plane_f(w(fz), sh)}, b2z, a2z);
+            tx = __builtin_elementwise_fma(f2{pv(nw[0]), pv(fw[0])}, b2x, a2x);
+            ty = __builtin_elementwise_fma(f2{pv(nw[1]), pv(fw[1])}, b2y, a2y);
+            tz = __builtin_elementwise_fma(f2{pv(nw[2]), pv(fw[2])}, b2z, a2z);
         }
         const float t0 = fmaxf(fmaxf(tx.x, ty.x), fmaxf(tz.x, 0.0f));
         const float t1 = fminf(fminf(tx.y, ty.y), fminf(tz.y, tcull));
@@ -1476,8 +1508,10 @@ template <int NW>
 __device__ __forceinline__ void node_slot_hits(const float4* np, v3 o, v3 inv, float tc, uint32_t slots, uint32_t& ih,
                                                uint32_t& lh, uint32_t& child_base, uint32_t& tri_base,
                                                uint32_t& counts, uint32_t& imask_out) {
-    const float4 f0 = np[0], f1 = np[1], qlx = np[2], qly = np[3], qlz = np[4], qhx = np[5], qhy = np[6],
-                 qhz = np[7];
+    float4 g[RT_NODE_F4];
+#pragma unroll
+    for (int k = 0; k < RT_NODE_F4; ++k) g[k] = np[k];
+    const float4 f0 = g[0], f1 = g[1];
     const uint32_t w3 = __float_as_uint(f0.w);
     const uint32_t imask = __float_as_uint(f1.z) & 0xFFu;
     const uint32_t lmask = (__float_as_uint(f1.z) >> 8) & 0xFFu;
@@ -1493,14 +1527,9 @@ __device__ __forceinline__ void node_slot_hits(const float4* np, v3 o, v3 inv, f
 #pragma unroll
     for (int s = 0; s < NW; ++s) {
         if (m & (1u << s)) {
-            const int wi = s >> 1, sh = (s & 1) * 16;
-            auto q = [&](const float4& f) {
-                const uint32_t wv = __float_as_uint(wi == 0 ? f.x : wi == 1 ? f.y : wi == 2 ? f.z : f.w);
-                return plane_f(wv, sh);
-            };
-            const float tlx = fmaf(q(qlx), bx, ax), thx = fmaf(q(qhx), bx, ax);
-            const float tly = fmaf(q(qly), by, ay), thy = fmaf(q(qhy), by, ay);
-            const float tlz = fmaf(q(qlz), bz, az), thz = fmaf(q(qhz), bz, az);
+            const float tlx = fmaf(node_plane(g, 0, s), bx, ax), thx = fmaf(node_plane(g, 3, s), bx, ax);
+            const float tly = fmaf(node_plane(g, 1, s), by, ay), thy = fmaf(node_plane(g, 4, s), by, ay);
+            const float tlz = fmaf(node_plane(g, 2, s), bz, az), thz = fmaf(node_plane(g, 5, s), bz, az);
             const float t0 = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fminf(tlz, thz));
             const float t1 = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fmaxf(tlz, thz));
             if (t0 <= t1 && t1 >= 0.0f && t0 <= tc) hits |= 1u << s;
@@ -1662,7 +1691,7 @@ __device__ __forceinline__ uint4 coop_group_trace(const float4* __restrict__ nod
         uint32_t ih = 0u, cb = 0u, imask = 0u;
         if (mine) {
             n.x++;
-            node_slot_hits<NW>(nodes + (size_t)(item >> 8) * 8, o, inv, any ? thr : tcull, item & 0xFFu, ih, lh, cb,
+            node_slot_hits<NW>(nodes + (size_t)(item >> 8) * RT_NODE_SF4, o, inv, any ? thr : tcull, item & 0xFFu, ih, lh, cb,
                                lb, lc, imask);
             rk = 0;
         }
@@ -2083,7 +2112,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_df_kernel(KParam
             tB = (unsigned long long)clock64();
             cnt.cyc_a += tB - tA;
         }
-        float4 g[8];
+        float4 g[RT_NODE_F4];
         if (PF && tracing && T.cur != RT_TRAV_NONE) node_fetch(S.nodes, T.cur, g);
         bool coop_now = false;
         for (;;) {
@@ -2713,7 +2742,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
             tB = (unsigned long long)clock64();
             cnt.cyc_a += tB - tA;
         }
-        float4 g[8];
+        float4 g[RT_NODE_F4];
         if (PF && tracing && T.cur != RT_TRAV_NONE) node_fetch(S.nodes, T.cur, g);
         bool to_coop = false;  // the loop ended for the lane groups (not for a partial refill)
         unsigned long long t_ph = 0ull;
@@ -3376,7 +3405,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_tree_kernel(KPar
             tB = (unsigned long long)clock64();
             cnt.cyc_a += tB - tA;
         }
-        float4 g[8];
+        float4 g[RT_NODE_F4];
         if (PF && tracing && T.cur != RT_TRAV_NONE) node_fetch(S.nodes, T.cur, g);
         for (;;) {
             if (COUNT) {

@@ -556,7 +556,7 @@ static int create_one(const rt_scene_desc* desc, int device, rt_ctx** out) {
         rt_destroy(c);
         return RT_ERR_INVALID;
     }
-    c->nnodes = gpu_built ? gbuild.nnodes : (int)(bvh8.nodes.size() / 32);
+    c->nnodes = gpu_built ? gbuild.nnodes : (int)(bvh8.nodes.size() / RT_NODE_SDW);
     if (c->nnodes >= (1 << 23)) c->df_ok = false;  // the DIRECT group stack's entries hold child_base << 9
     c->nrec = ntri;
 
@@ -1040,12 +1040,24 @@ static bool fans_pay(const rt_ctx* c, const KParams& K) {
     return (ns >= 16 && ns <= 64) || (np >= 16 && np <= 64);
 }
 
-// the kernel class a render runs: whole-traversal refill for small scenes, dynamic fetch for large ones
-// and for sample-heavy lights
+// the scene's pixels can be drawn by the opaque-scene or the recursion-tree kernel (opaque_path / tree_path
+// without the class test): no textures, no glossy lobes, sample fans within a wave
+static bool lite_eligible(const rt_ctx* c, const KParams& K) {
+    if (c->opt_variant >= 0 || K.S.tex_on || !(K.glossy_n == 1 || !c->glossy_material)) return false;
+    const bool opaque = c->opt_opaque != 0 && K.S.all_opaque && K.S.nsl == 0 && K.S.nplane == 0;
+    const bool tree = c->opt_tree != 0 && c->opt_fan && (K.S.nsl == 0 || 1 + K.sl_m * K.sl_n <= 64) &&
+                      (K.S.nplane == 0 || K.plane_k * K.plane_k <= 64) &&
+                      (long long)K.S.npl + K.S.nsl + K.S.nspot + K.S.nplane < 65536;
+    return opaque || tree;
+}
+
+// the kernel class a render runs: dynamic fetch for large scenes, sample-heavy lights and every scene the opaque or
+// recursion-tree kernel draws (round 6: C2 64-view batch 0.268 -> 0.109 ms/frame, frame 0.626 -> 0.38-0.50 ms;
+// profiles/r06/ab_r06e.log); whole-traversal refill for the small scenes left (textures, glossy lobes)
 static bool use_df(const rt_ctx* c, const KParams& K) {
     if (!c->df_ok || c->opt_kernel == RT_KERNEL_WHOLE_TRAVERSAL) return false;
     if (c->opt_kernel == RT_KERNEL_DYNAMIC_FETCH) return true;
-    return c->ntri >= RT_DF_MIN_TRIANGLES || fans_pay(c, K);
+    return c->ntri >= RT_DF_MIN_TRIANGLES || fans_pay(c, K) || lite_eligible(c, K);
 }
 
 // Kernel variants compiled (rt_megakernel.hip RT_V_*).  The dynamic-fetch class ships two, chosen by
@@ -1602,7 +1614,7 @@ static int launch_wavefront(rt_ctx* c, KParams& K, hipStream_t st, rt_stats* sta
         float ms = 0.0f;
         HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
         stats->kernel_ms = ms;
-        stats->node_bytes = 128u;
+        stats->node_bytes = RT_NODE_DW * 4u;
         std::memcpy(stats->kernel, c->last_kernel, sizeof(stats->kernel));
         stats->kernel[sizeof(stats->kernel) - 1] = 0;
     }
@@ -1676,7 +1688,7 @@ static int launch_render(rt_ctx* c, KParams& K, hipStream_t st, int count_mode, 
         float ms = 0.0f;
         if (blocks > 0) HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
         stats->kernel_ms = ms;
-        stats->node_bytes = 128u;  // quantised BVH8 node
+        stats->node_bytes = RT_NODE_DW * 4u;  // quantised BVH8 node
         std::memcpy(stats->kernel, c->last_kernel, sizeof(stats->kernel));
         stats->kernel[sizeof(stats->kernel) - 1] = 0;
     }

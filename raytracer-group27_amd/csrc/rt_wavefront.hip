@@ -145,7 +145,7 @@ __global__ __launch_bounds__(64, WV & 15) void wf_trace_kernel(KParams, WfBufs) 
     }
     Trav T;
     trav_idle(T);
-    float4 g[8];  // PF: the node the lane visits next
+    float4 g[RT_NODE_F4];  // PF: the node the lane visits next
     Cnt cnt{};
     int src = -1;       // the query this lane traces: < n_path a path ray (camera job), else a segment
     uint32_t tag = 0u;  // a segment's shading point << 5 | light; a camera ray's output pixel

@@ -10,10 +10,16 @@ import numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def _codec(tmp_path, u8):
+    exe = str(tmp_path / f"plane_codec_u8{u8}")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", f"-DRT_PLANES_U8={u8}", "-I",
+                    os.path.join(REPO, "raytracer-group27_amd", "csrc"), os.path.join(REPO, "tests", "cpp", "plane_codec.cpp"),
+                    "-o", exe], check=True)
+    return exe
+
+
 def test_plane_words_are_conservative_halves(tmp_path):
-    exe = str(tmp_path / "plane_codec")
-    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-I", os.path.join(REPO, "raytracer-group27_amd",
-                    "csrc"), os.path.join(REPO, "tests", "cpp", "plane_codec.cpp"), "-o", exe], check=True)
+    exe = _codec(tmp_path, 0)
     rng = np.random.default_rng(16)
     xs = np.concatenate([[0.0, 1e-9, 6e-8, 1.0, 2047.5, 2048.0, 2049.0, 65000.0, 65504.0, 70000.0],
                          rng.uniform(0, 65504, 4000), rng.uniform(0, 2, 2000), 2.0 ** rng.uniform(-24, 16, 2000)])
@@ -35,3 +41,23 @@ def test_plane_words_are_conservative_halves(tmp_path):
                 assert float(np.array([u - 1], np.uint16).view(np.float16)[0]) < x, (x, u)
         else:
             assert d == u == 0x7BFF
+
+
+def test_plane_bytes_are_conservative_steps(tmp_path):
+    """RT_PLANES_U8 (80-B nodes): a plane is an 8-bit step count, the lo plane rounded down and the hi plane up to
+    the integer grid, clamped to 0..255 -- floor / ceil exactly (the builders pick the exponent so a child's
+    offsets fit 255 steps)."""
+    exe = _codec(tmp_path, 1)
+    rng = np.random.default_rng(8)
+    xs = np.concatenate([[0.0, 1e-9, 0.5, 1.0, 254.0, 254.5, 255.0, 255.25, 300.0], rng.uniform(0, 255, 4000),
+                         rng.uniform(0, 2, 1000)])
+    out = subprocess.run([exe], input="\n".join(repr(float(x)) for x in xs), capture_output=True, text=True,
+                         check=True).stdout.split("\n")
+    for x, line in zip(xs, out):
+        d, u, vd, vu = line.split()
+        d, u, vd, vu = int(d), int(u), float(vd), float(vu)
+        assert (vd, vu) == (d, u)
+        if x <= 255.0:
+            assert d == int(np.floor(x)) and u == int(np.ceil(x)), (x, d, u)
+        else:
+            assert d == u == 255

@@ -72,5 +72,6 @@ for cfg in args.configs:
         same = "bits = arm 1" if sums[name] == sums[arms[0][0]] and rays[name][1] == rays[arms[0][0]][1] else \
             "BITS DIFFER from arm 1"
         print(f"{cfg} {name:>10}: frame {f:7.3f} ms ({r1 / f / 1e3:7.1f} Mrays/s)  batch {b:7.3f} ms/frame "
-              f"({rv / args.views / b / 1e3:7.1f} Mrays/s)  [{kn}] {same}", flush=True)
+              f"({rv / args.views / b / 1e3:7.1f} Mrays/s)  [{kn}] {same} rays {rv} sum {sums[name][0]:x}.{sums[name][1] & 0xFFFFFFFF:x}",
+              flush=True)
     ctx.close()

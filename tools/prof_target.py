@@ -2,12 +2,15 @@
 times: one frame (views = 1) or a turntable batch of V views in one launch (bench.py --views V), every pixel
 stored in its setPixel place (rt_render_views_image_device).
 
-    python tools/prof_target.py CONFIG N [VIEWS]      (PT_OPTS="16=1" selects render-path options)
+    python tools/prof_target.py CONFIG N [VIEWS]      (PT_OPTS="16=1" selects render-path options; PT_LIB=path another
+                                                       build of the library)
 """
 import os, sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "raytracer-group27_amd"))
 import rt_amd as R
+if os.environ.get("PT_LIB"):  # another build of the library (developer A/B of builds under the profiler)
+    R.LIB_PATH = os.path.abspath(os.environ["PT_LIB"])
 cfg = sys.argv[1] if len(sys.argv) > 1 else "C3"
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 views = int(sys.argv[3]) if len(sys.argv) > 3 else 1
