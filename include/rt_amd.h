@@ -391,7 +391,7 @@ int rt_debug_counters(rt_ctx* ctx, uint64_t* out, int n);
 #define RT_OPT_DUAL_STEP 10  /* dynamic-fetch kernel: a lane testing leaf records also visits its next node in the same step (-1 default = 1, 0 off) */
 #define RT_OPT_CENTRE_FIRST 12 /* job order: the per-XCD tile ranges above the image centre walked bottom-up, so every range starts at its rows nearest the centre: -1 by render shape, 0 off, 1 on */
 #define RT_OPT_OPAQUE 11     /* opaque-scene kernel (opaque materials, point / spot lights, no lobes or textures): -1 where eligible (the 4-wave build; with one light, its SPLIT form: shadow segments traced beside the mirror chain), 0 never, 1 the 4-wave build without SPLIT, 2 the 3-wave build, 3 the 4-wave build with the re-visit group stack, 4 / 5 SPLIT at 4 / 3 waves, 6 / 7 SPLIT without drain lane groups at 5 / 4 waves (A/Bs; SPLIT options fall back to 1 on scenes with more lights) */
-#define RT_OPT_TREE 13       /* recursion-tree kernel (transparent materials, all four light types with <= 64-sample fans, no lobes or textures): -1 / 2 where eligible, 0 never, 1 its build with the re-visit group stack (A/B), 3 a checked 4-wave build (developer diagnosis: out-of-range indices reported in rt_debug_counters [24] / [25] instead of accessed) */
+#define RT_OPT_TREE 13       /* recursion-tree kernel (transparent materials, all four light types with <= 64-sample fans, no lobes or textures): -1 / 2 where eligible (4-wave build for view batches, 3-wave for single frames), 0 never, 1 its build with the re-visit group stack (A/B), 3 a checked 4-wave build (developer diagnosis: out-of-range indices reported in rt_debug_counters [24] / [25] instead of accessed), 4 / 5 the 4- / 3-wave build for every render */
 #define RT_OPT_PEER_STORES 14 /* split renders: -1 the replicas with peer access to devices[0] store their pixels straight into its images (default), 0 every replica renders band-dense on its own device and copies (the path of devices without peer access) */
 #define RT_OPT_INTERLEAVE_TAIL 15 /* opaque-kernel view batches: the last n views' jobs spread over 16 tiles per wave (the launch's drain), the others in tile order; 0 none (the default: measured slower) */
 #define RT_OPT_WAVEFRONT 16   /* opaque-kernel scenes with one camera sample per pixel: -1 (default) and 0 the persistent opaque megakernel (no render shape is faster on the wavefront path), 1 the wavefront path (rt_wavefront.hip: a lean trace kernel per recursion level and an elementwise shade kernel between; bit-identical images), 2..64 the wavefront path with this trace-kernel refill threshold (A/B) */

@@ -26,6 +26,11 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("RT_OFFLOAD_ARCH", "gfx950")
 
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-function"]
+# HIP sources: every automatic variable defined at its declaration.  The kernels read no variable before writing it
+# (the clang static analyzer, -Wuninitialized and the machine verifier find nothing), but their optimised IR keeps
+# undef values on paths that do not use them, and the 4-wave recursion-tree build that faulted in rounds 4-5 ran the
+# faulting C4 batch green once built this way (profiles/r06/fault/): no kernel is compiled with undefs
+HIP_FLAGS = ["-ftrivial-auto-var-init=pattern"]
 
 
 def _sources():
@@ -119,7 +124,7 @@ def build(force=False, verbose_resource=False, defines=(), out=None):
         obj = os.path.join(BUILD, s + ".o")
         if force or _stale(src, obj, headers):
             extra = ["-Rpass-analysis=kernel-resource-usage"] if verbose_resource else []
-            jobs.append([HIPCC, "-x", "hip", f"--offload-arch={ARCH}"] + COMMON + extra_d + ["-Wno-unused-result",
+            jobs.append([HIPCC, "-x", "hip", f"--offload-arch={ARCH}"] + COMMON + HIP_FLAGS + extra_d + ["-Wno-unused-result",
                         "-Wno-unused-value"] + extra + ["-c", src, "-o", obj])
         objs.append(obj)
     # the provenance stamp: one generated translation unit holding the source hash

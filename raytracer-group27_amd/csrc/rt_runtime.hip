@@ -107,7 +107,7 @@ struct rt_ctx {
     bool glossy_material = false;  // opaque, ks > 0, shininess != 0 (glossy_ray_count > 1 draws lobes)
     int persistent_blocks[1024] = {0};  // resident 64-lane blocks per (kernel class, variant)
     int opaque_blocks[6] = {0, 0, 0, 0, 0, 0};  // ... of the opaque-scene kernel (4 / 3 waves per SIMD; SPLIT; A/Bs)
-    int tree_blocks[3] = {0, 0, 0};     // ... of the recursion-tree kernel (3-wave, re-visit, checked 4-wave)
+    int tree_blocks[4] = {0, 0, 0, 0};  // ... of the recursion-tree kernel (3-wave, re-visit, checked 4-wave, 4-wave)
     // recursion-tree kernel: the lanes' pending refracted rays (KParams::frames)
     float* d_frames = nullptr;
     float4* d_plane_tab = nullptr;  // plane lights: their sample grids and normals (KParams::plane_tab)
@@ -979,7 +979,7 @@ static int set_option_one(rt_ctx* c, int option, int value) {
             c->opt_opaque = value;
             return RT_OK;
         case RT_OPT_TREE:
-            if (value < -1 || value > 3) break;
+            if (value < -1 || value > 5) break;
             c->opt_tree = value;
             return RT_OK;
         case RT_OPT_PEER_STORES:
@@ -1109,12 +1109,15 @@ static int opaque_variant(const rt_ctx* c, const KParams& K) {
 }
 
 // the recursion-tree kernel (rt_megakernel.hip persistent_tree_kernel): 4 / 3 waves per SIMD
-// One build, 3 waves per SIMD, for frames and batches: the 4-wave build (67 spilled VGPRs) faulted on the
-// C4 16-view batch at full size (round 4, gpurun_out/bench_r04b_C4.json) and is not compiled.
+// View batches run the 4-wave build, single frames the 3-wave one (round 6: C4 16-view batch 6.77-6.82 -> 6.09-6.13
+// ms/frame, C4 frame 6.92-6.95 vs 7.32-7.57 ms at 4 waves; profiles/r06/ab_r06k*.log).  The 4-wave build faulted
+// in rounds 4-5 when compiled with undef values in its IR; with every automatic variable defined (build.py
+// HIP_FLAGS) it runs every size bit-identically.
 #define RT_TREE_V3 (RT_V_W3 | RT_V_NOPF)
 #define RT_TREE_VR (RT_V_W3 | RT_V_NOPF | RT_V_REVISIT)  // A/B: the re-visit group stack (RT_OPT_TREE 1)
 // developer diagnosis of the 4-wave build's fault (RT_OPT_TREE 3): that build with every index checked (RT_V_CHK)
 #define RT_TREE_V4C (RT_V_W4 | RT_V_NOPF | RT_V_CHK)
+#define RT_TREE_V4 (RT_V_W4 | RT_V_NOPF)  // view batches (RT_OPT_TREE 4 forces it, 5 forces the 3-wave build)
 
 // Renders that the recursion-tree kernel draws: pixels of a dynamic-fetch-class render the opaque kernel
 // does not take, without textures or glossy lobes, whose spherical and plane lights fit one fan (<= 64
@@ -1127,8 +1130,12 @@ static bool tree_path(const rt_ctx* c, const KParams& K, bool pixels) {
     if (K.S.nplane > 0 && K.plane_k * K.plane_k > 64) return false;
     return (long long)K.S.npl + K.S.nsl + K.S.nspot + K.S.nplane < 65536;  // TreeLane::li
 }
-static int tree_variant(const rt_ctx* c) {
-    return c->opt_tree == 1 ? RT_TREE_VR : c->opt_tree == 3 ? RT_TREE_V4C : RT_TREE_V3;
+static int tree_variant(const rt_ctx* c, const KParams& K) {
+    if (c->opt_tree == 1) return RT_TREE_VR;
+    if (c->opt_tree == 3) return RT_TREE_V4C;
+    if (c->opt_tree == 4) return RT_TREE_V4;
+    if (c->opt_tree == 5) return RT_TREE_V3;
+    return K.n_views > 1 ? RT_TREE_V4 : RT_TREE_V3;
 }
 
 // by render shape: view batches and sample-fan renders run the lean 4-wave variant (C4 single frame
@@ -1183,9 +1190,10 @@ static int launch_persistent(int grid, hipStream_t st, const KParams& K, const J
         return RT_OK;
     }
     if (tree_path(c, K, J.mode == 0)) {
-        const int v = tree_variant(c);
+        const int v = tree_variant(c, K);
         if (v == RT_TREE_VR) hipLaunchKernelGGL((persistent_tree_kernel<COUNT, RT_TREE_VR>), dim3(grid), dim3(64), 0, st, K, J);
         else if (v == RT_TREE_V4C) hipLaunchKernelGGL((persistent_tree_kernel<COUNT, RT_TREE_V4C>), dim3(grid), dim3(64), 0, st, K, J);
+        else if (v == RT_TREE_V4) hipLaunchKernelGGL((persistent_tree_kernel<COUNT, RT_TREE_V4>), dim3(grid), dim3(64), 0, st, K, J);
         else hipLaunchKernelGGL((persistent_tree_kernel<COUNT, RT_TREE_V3>), dim3(grid), dim3(64), 0, st, K, J);
         std::snprintf(c->last_kernel, sizeof(c->last_kernel), "rt::persistent_tree_kernel<%s, %d>",
                       COUNT ? "true" : "false", v);
@@ -1239,12 +1247,14 @@ static int persistent_grid(rt_ctx* c, const KParams& K, bool pixels) {
         return c->opaque_blocks[key];
     }
     if (tree_path(c, K, pixels)) {
-        const int key = tree_variant(c) == RT_TREE_VR ? 1 : tree_variant(c) == RT_TREE_V4C ? 2 : 0;
+        const int tv = tree_variant(c, K);
+        const int key = tv == RT_TREE_VR ? 1 : tv == RT_TREE_V4C ? 2 : tv == RT_TREE_V4 ? 3 : 0;
         if (c->tree_blocks[key] > 0) return c->tree_blocks[key];
         int cus = 0, per_cu = 0;
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
         const hipError_t e =
-            key == 1   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_tree_kernel<false, RT_TREE_VR>, 64, 0)
+            key == 3   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_tree_kernel<false, RT_TREE_V4>, 64, 0)
+            : key == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_tree_kernel<false, RT_TREE_VR>, 64, 0)
             : key == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_tree_kernel<false, RT_TREE_V4C>, 64, 0)
                        : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_tree_kernel<false, RT_TREE_V3>, 64, 0);
         if (e != hipSuccess || per_cu <= 0) per_cu = 8;

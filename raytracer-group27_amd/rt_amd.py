@@ -157,7 +157,7 @@ OPT_DUAL_STEP = 10
 OPT_CENTRE_FIRST = 12  # job order: upper-half XCD tile ranges walked bottom-up (-1 by shape, 0 off, 1 on)
 OPT_OPAQUE = 11  # opaque-scene kernel: -1 where eligible (default: 4-wave, SPLIT with one light), 0 the general kernels, 1 4-wave without SPLIT, 2 3-wave, 3 re-visit, 4 / 5 SPLIT 4- / 3-wave, 6 / 7 SPLIT without lane groups 5- / 4-wave (A/Bs)
 OPT_PEER_STORES = 14  # split renders: -1 peer stores where peer access works (default), 0 band-dense + copy always
-OPT_TREE = 13  # recursion-tree kernel (C4 / C5 class): -1 / 2 where eligible (default), 0 the general kernels, 1 its re-visit group stack build (A/B), 3 a checked 4-wave build
+OPT_TREE = 13  # recursion-tree kernel (C4 / C5 class): -1 / 2 where eligible (default: 4 waves for batches, 3 for frames), 0 the general kernels, 1 its re-visit group stack build (A/B), 3 a checked 4-wave build, 4 / 5 the 4- / 3-wave build always
 OPT_INTERLEAVE_TAIL = 15  # opaque batches: the last n views interleaved over 16 tiles (0 none)
 OPT_WF_STREAMS = 18  # wavefront chunks over 1..4 streams (0: default 2)
 OPT_PRIO = 19  # opaque kernel: s_setprio 2 after this many iterations of a traversal phase (-1 by shape, 0 never)

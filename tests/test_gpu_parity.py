@@ -416,6 +416,30 @@ def test_plane_and_transparent_fans_match_oracle(R, O):
         ctx.close()
 
 
+def test_c4_full_size_batch_four_wave_tree(R, ctxs):
+    """The batch that faulted the 4-wave recursion-tree build in rounds 4-5: C4 at 1920x1080, a 16-view turntable in
+    one launch.  The shipped batch build (4 waves, every automatic variable defined: build.py HIP_FLAGS) renders the
+    same bits and ray count as the 3-wave build (RT_OPT_TREE 5) and as single frames of the same cameras."""
+    import torch
+
+    scene, ctx, prm, W, H = ctxs("C4")
+    F = 16
+    cams = R.turntable_cameras(F, R.aspect_of(W, H))
+    out = {}
+    for tree in (-1, 5):
+        buf = torch.full((F * W * H * 3,), -1.0, dtype=torch.float32, device="cuda")
+        with V.options(R, ctx, {R.OPT_TREE: tree}):
+            st = ctx.render_views_image_device(cams, prm, W, H, buf.data_ptr(), None)
+        torch.cuda.synchronize()
+        out[tree] = (buf, st.rays, st.kernel_name)
+    assert "persistent_tree_kernel<false, 18>" in out[-1][2], out[-1][2]
+    assert "persistent_tree_kernel<false, 10>" in out[5][2], out[5][2]
+    assert out[-1][1] == out[5][1]
+    assert torch.equal(out[-1][0], out[5][0])
+    one, _ = ctx.render(cams[5], prm, W, H)
+    assert out[-1][0].view(F, -1)[5].cpu().numpy().tobytes() == one.tobytes()
+
+
 def test_bench_step_c3_64_views(R, O, ctxs):
     """The benchmarked step itself (bench.py defaults): C3 at 1920x1080, a 64-view turntable in ONE
     rt_render_views_device launch, rebuilt by rt_unpermute_views_device.  Views 0, 21 and 63 are

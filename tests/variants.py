@@ -47,6 +47,8 @@ def all_variants(R):
         {R.OPT_KERNEL: df, R.OPT_TREE: 1},                      # the tree kernel with the re-visit group stack
         {R.OPT_KERNEL: df, R.OPT_TREE: 2},                      # ... and with the direct one (its default)
         {R.OPT_KERNEL: df, R.OPT_TREE: 3},                      # ... its 4-wave build with every index checked
+        {R.OPT_KERNEL: df, R.OPT_TREE: 4},                      # ... its 4-wave build (view batches' default)
+        {R.OPT_KERNEL: df, R.OPT_TREE: 5},                      # ... its 3-wave build (single frames' default)
         {R.OPT_KERNEL: df, R.OPT_WAVEFRONT: 0},                 # the opaque megakernel where the wavefront is eligible
         {R.OPT_KERNEL: df, R.OPT_WAVEFRONT: 1},                 # the wavefront path (trace / shade kernels)
         {R.OPT_KERNEL: df, R.OPT_WAVEFRONT: 2},                 # ... its trace kernel refilling at 2 waiting lanes
