@@ -1084,7 +1084,11 @@ static bool use_df(const rt_ctx* c, const KParams& K) {
 // textures and without glossy lobes (glossy_ray_count 1, or no glossy material).  RT_OPT_OPAQUE 0 and any
 // RT_OPT_VARIANT choice select the general kernels instead.
 static bool use_df(const rt_ctx* c, const KParams& K);
+static bool split_ok(const KParams& K);
 static bool opaque_path(const rt_ctx* c, const KParams& K, bool pixels) {
+    // (small scenes with more than one light: the recursion-tree kernel draws them faster -- C2 64-view batch 0.104
+    // vs 0.100 ms/frame, frame 0.459 vs 0.376 ms, profiles/r06/ab_r06m.log -- unless RT_OPT_OPAQUE asks for it)
+    if (c->opt_opaque < 0 && c->ntri < RT_DF_MIN_TRIANGLES && !split_ok(K)) return false;
     return pixels && c->opt_opaque != 0 && c->opt_variant < 0 && use_df(c, K) && K.S.all_opaque && K.S.nsl == 0 &&
            K.S.nplane == 0 && !K.S.tex_on && (K.glossy_n == 1 || !c->glossy_material);
 }
@@ -1100,6 +1104,10 @@ static bool opaque_path(const rt_ctx* c, const KParams& K, bool pixels) {
 #define RT_OPAQUE_V4SN (RT_V_W4 | RT_V_NOPF | RT_V_NOCOOP | RT_V_SPLIT)  // A/B: 4 waves, no drain lane groups
 static bool split_ok(const KParams& K) { return K.S.npl + K.S.nspot == 1 && K.max_level < 16; }
 static int opaque_variant(const rt_ctx* c, const KParams& K) {
+    // view batches with SPLIT: 5 waves per SIMD without the drain lane groups (round 6, every automatic variable
+    // defined: 20 spilled VGPRs instead of 33; C3 64-view batch 0.372 -> 0.352 ms/frame, profiles/r06/ab_r06m.log);
+    // single frames keep the 4-wave build with the lane groups (1.13 vs 0.92 ms without them)
+    if (c->opt_opaque == -1 && K.n_views > 1 && split_ok(K)) return RT_OPAQUE_V5S;
     if (c->opt_opaque == 2) return RT_OPAQUE_V3;
     if (c->opt_opaque == 3) return RT_OPAQUE_V | RT_V_REVISIT;
     if (c->opt_opaque == 1 || !split_ok(K)) return RT_OPAQUE_V;
@@ -1182,6 +1190,7 @@ static int launch_persistent(int grid, hipStream_t st, const KParams& K, const J
             hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V5S>), dim3(grid), dim3(64), 0, st, K, J);
         } else if (v == RT_OPAQUE_V4SN) {
             hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V4SN>), dim3(grid), dim3(64), 0, st, K, J);
+
         } else {
             hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V>), dim3(grid), dim3(64), 0, st, K, J);
         }
