@@ -1019,6 +1019,7 @@ __device__ __attribute__((noinline)) bool advance_lane_call(const void* ka, Lane
 #define RT_V_SPLIT 128   // opaque kernel: a node's shadow segment traced beside its mirror child (split_node)
 #define RT_V_W5 512      // opaque kernel: compiled for 5 waves per SIMD (96 VGPRs; with NOCOOP its LDS fits 20 blocks)
 #define RT_V_WAVES(V) (((V) & RT_V_W5) ? 5 : ((V) & RT_V_W4) ? 4 : ((V) & RT_V_W3) ? 3 : 2)
+#define RT_V_OVL 1024    // opaque kernel: a dual step's node loads issued before its record test (A/B)
 
 // the ray mix of counting builds: a query starts (a cansee segment or light sample, or a camera ray: level 0, not a
 // segment) and ends (a camera ray that found nothing)
@@ -2520,7 +2521,7 @@ __device__ __forceinline__ v3 split_fold(const KParams& P, const SplitLane& L, i
 template <bool COUNT, int V>
 __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KParams, JobSrc) {
     constexpr bool PF = !(V & RT_V_NOPF), COOP = !(V & RT_V_NOCOOP), DIRECT = !(V & RT_V_REVISIT);
-    constexpr bool SPLIT = (V & RT_V_SPLIT) != 0;
+    constexpr bool SPLIT = (V & RT_V_SPLIT) != 0, OVL = (V & RT_V_OVL) != 0;
     // the kernel's arguments are read where each phase uses them (fresh_kernarg), not held in SGPRs
     const void* ka = (const void*)__builtin_amdgcn_kernarg_segment_ptr();
 #define RT_FRESH const KParams& P = *(const KParams*)fresh_kernarg(ka); const DevScene& S = P.S
@@ -2762,6 +2763,12 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
             }
             if (tracing) {
                 const bool rec = leaf_pending(T);
+                if constexpr (OVL) {
+                    // the node this step visits, decided before the record test (it only pops the next hit leaf, or
+                    // ends an any-hit query: then the node was loaded for nothing), so both round trips overlap
+                    const uint32_t lh_after = (rec && T.rk == 0) ? (T.lh & (T.lh - 1u)) : T.lh;
+                    if (T.cur != RT_TRAV_NONE && (!rec || (P.dual && lh_after == 0u))) node_fetch(S.nodes, T.cur, g);
+                }
                 if (rec) trav_record<COUNT, true, false, true>(S, T, cnt, nullptr, COUNT ? &slab : nullptr, &ref_lds);
                 if (COUNT) {  // the wave's ref_slab executions this step: the most any lane did
                     const uint32_t ns = rec ? slab.step : 0u;
@@ -2775,7 +2782,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
                     if (nv && rec) slab.both++;
                     if (!nv && T.cur != RT_TRAV_NONE) slab.blocked++;
                 }
-                if (nv) trav_node<COUNT, 8, PF, DIRECT>(S, T, stk, g, cnt);
+                if (nv) trav_node<COUNT, 8, PF && !OVL, DIRECT, false, OVL>(S, T, stk, g, cnt);
             }
             if (tracing && !leaf_pending(T) && T.cur == RT_TRAV_NONE) {
                 trav_finish(S, T);

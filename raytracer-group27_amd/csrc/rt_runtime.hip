@@ -106,7 +106,7 @@ struct rt_ctx {
     bool df_ok = true;  // the BVH8 fits the dynamic-fetch kernel's LDS stack
     bool glossy_material = false;  // opaque, ks > 0, shininess != 0 (glossy_ray_count > 1 draws lobes)
     int persistent_blocks[1024] = {0};  // resident 64-lane blocks per (kernel class, variant)
-    int opaque_blocks[6] = {0, 0, 0, 0, 0, 0};  // ... of the opaque-scene kernel (4 / 3 waves per SIMD; SPLIT; A/Bs)
+    int opaque_blocks[7] = {0, 0, 0, 0, 0, 0, 0};  // ... of the opaque-scene kernel (4 / 3 waves per SIMD; SPLIT; A/Bs)
     int tree_blocks[4] = {0, 0, 0, 0};  // ... of the recursion-tree kernel (3-wave, re-visit, checked 4-wave, 4-wave)
     // recursion-tree kernel: the lanes' pending refracted rays (KParams::frames)
     float* d_frames = nullptr;
@@ -975,7 +975,7 @@ static int set_option_one(rt_ctx* c, int option, int value) {
             c->opt_variant = value;
             return RT_OK;
         case RT_OPT_OPAQUE:
-            if (value < -1 || value > 7) break;
+            if (value < -1 || value > 8) break;
             c->opt_opaque = value;
             return RT_OK;
         case RT_OPT_TREE:
@@ -1102,6 +1102,7 @@ static bool opaque_path(const rt_ctx* c, const KParams& K, bool pixels) {
 // drain lane groups at 5 / 4 waves (A/Bs: 0.388 / 0.377 ms/frame, frames 1.26 / 1.14 ms)
 #define RT_OPAQUE_V5S (RT_V_W5 | RT_V_NOPF | RT_V_NOCOOP | RT_V_SPLIT)   // A/B: 5 waves, no drain lane groups
 #define RT_OPAQUE_V4SN (RT_V_W4 | RT_V_NOPF | RT_V_NOCOOP | RT_V_SPLIT)  // A/B: 4 waves, no drain lane groups
+#define RT_OPAQUE_V5SO (RT_OPAQUE_V5S | RT_V_OVL)  // A/B: the batch build with a dual step's loads overlapped
 static bool split_ok(const KParams& K) { return K.S.npl + K.S.nspot == 1 && K.max_level < 16; }
 static int opaque_variant(const rt_ctx* c, const KParams& K) {
     // view batches with SPLIT: 5 waves per SIMD without the drain lane groups (round 6, every automatic variable
@@ -1113,6 +1114,7 @@ static int opaque_variant(const rt_ctx* c, const KParams& K) {
     if (c->opt_opaque == 1 || !split_ok(K)) return RT_OPAQUE_V;
     if (c->opt_opaque == 6) return RT_OPAQUE_V5S;
     if (c->opt_opaque == 7) return RT_OPAQUE_V4SN;
+    if (c->opt_opaque == 8) return RT_OPAQUE_V5SO;
     return (c->opt_opaque == 5 ? RT_OPAQUE_V3 : RT_OPAQUE_V) | RT_V_SPLIT;
 }
 
@@ -1190,6 +1192,8 @@ static int launch_persistent(int grid, hipStream_t st, const KParams& K, const J
             hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V5S>), dim3(grid), dim3(64), 0, st, K, J);
         } else if (v == RT_OPAQUE_V4SN) {
             hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V4SN>), dim3(grid), dim3(64), 0, st, K, J);
+        } else if (v == RT_OPAQUE_V5SO) {
+            hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V5SO>), dim3(grid), dim3(64), 0, st, K, J);
 
         } else {
             hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V>), dim3(grid), dim3(64), 0, st, K, J);
@@ -1240,12 +1244,13 @@ static int occupancy_of(int* per_cu) {
 static int persistent_grid(rt_ctx* c, const KParams& K, bool pixels) {
     if (opaque_path(c, K, pixels)) {
         const int v = opaque_variant(c, K);
-        const int key = v == RT_OPAQUE_V5S ? 4 : v == RT_OPAQUE_V4SN ? 5 : ((v & RT_V_W3) ? 1 : 0) + ((v & RT_V_SPLIT) ? 2 : 0);
+        const int key = v == RT_OPAQUE_V5SO ? 6 : v == RT_OPAQUE_V5S ? 4 : v == RT_OPAQUE_V4SN ? 5 : ((v & RT_V_W3) ? 1 : 0) + ((v & RT_V_SPLIT) ? 2 : 0);
         if (c->opaque_blocks[key] > 0) return c->opaque_blocks[key];
         int cus = 0, per_cu = 0;
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
         const hipError_t e =
-            key == 5   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V4SN>, 64, 0)
+            key == 6   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V5SO>, 64, 0)
+            : key == 5 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V4SN>, 64, 0)
             : key == 4 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V5S>, 64, 0)
             : key == 3 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V3 | RT_V_SPLIT>, 64, 0)
             : key == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V | RT_V_SPLIT>, 64, 0)
