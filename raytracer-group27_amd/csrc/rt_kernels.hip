@@ -169,6 +169,9 @@ struct Cnt {
     uint32_t rv, rvk, rvj;
     // the ray mix (counting builds): cansee segments and light samples, camera queries that hit nothing
     uint32_t shad, cmiss;
+    // the tree kernel's phase A in parts (counting builds, wave leader): finished samples and segments, owners
+    // resuming and advancing, the fan hand-out
+    unsigned long long cyc_e, cyc_f, cyc_g;
 };
 
 // reference-box tests of candidate culling (ref_slab): lane evaluations, the wave's executions (the most any lane
@@ -709,6 +712,11 @@ __device__ void flush_counters(const KParams& P, const Cnt& c) {
             unsigned long long v = xs[k];
             for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
             if ((threadIdx.x & 63) == 0) atomicAdd(P.stats + RT_STATS_EXTRA + k, v);
+        }
+        if ((threadIdx.x & 63) == 0) {  // rt_debug_counters [50], [51], [52]
+            atomicAdd(P.stats + RT_STATS_EXTRA + 16, c.cyc_e);
+            atomicAdd(P.stats + RT_STATS_EXTRA + 17, c.cyc_f);
+            atomicAdd(P.stats + RT_STATS_EXTRA + 18, c.cyc_g);
         }
         const uint32_t mix[2] = {c.shad, c.cmiss};  // rt_debug_counters [26], [27]
         for (int k = 0; k < 2; ++k) {

@@ -1019,7 +1019,6 @@ __device__ __attribute__((noinline)) bool advance_lane_call(const void* ka, Lane
 #define RT_V_SPLIT 128   // opaque kernel: a node's shadow segment traced beside its mirror child (split_node)
 #define RT_V_W5 512      // opaque kernel: compiled for 5 waves per SIMD (96 VGPRs; with NOCOOP its LDS fits 20 blocks)
 #define RT_V_WAVES(V) (((V) & RT_V_W5) ? 5 : ((V) & RT_V_W4) ? 4 : ((V) & RT_V_W3) ? 3 : 2)
-#define RT_V_OVL 1024    // opaque kernel: a dual step's node loads issued before its record test (A/B)
 
 // the ray mix of counting builds: a query starts (a cansee segment or light sample, or a camera ray: level 0, not a
 // segment) and ends (a camera ray that found nothing)
@@ -2521,7 +2520,7 @@ __device__ __forceinline__ v3 split_fold(const KParams& P, const SplitLane& L, i
 template <bool COUNT, int V>
 __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KParams, JobSrc) {
     constexpr bool PF = !(V & RT_V_NOPF), COOP = !(V & RT_V_NOCOOP), DIRECT = !(V & RT_V_REVISIT);
-    constexpr bool SPLIT = (V & RT_V_SPLIT) != 0, OVL = (V & RT_V_OVL) != 0;
+    constexpr bool SPLIT = (V & RT_V_SPLIT) != 0;
     // the kernel's arguments are read where each phase uses them (fresh_kernarg), not held in SGPRs
     const void* ka = (const void*)__builtin_amdgcn_kernarg_segment_ptr();
 #define RT_FRESH const KParams& P = *(const KParams*)fresh_kernarg(ka); const DevScene& S = P.S
@@ -2763,12 +2762,6 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
             }
             if (tracing) {
                 const bool rec = leaf_pending(T);
-                if constexpr (OVL) {
-                    // the node this step visits, decided before the record test (it only pops the next hit leaf, or
-                    // ends an any-hit query: then the node was loaded for nothing), so both round trips overlap
-                    const uint32_t lh_after = (rec && T.rk == 0) ? (T.lh & (T.lh - 1u)) : T.lh;
-                    if (T.cur != RT_TRAV_NONE && (!rec || (P.dual && lh_after == 0u))) node_fetch(S.nodes, T.cur, g);
-                }
                 if (rec) trav_record<COUNT, true, false, true>(S, T, cnt, nullptr, COUNT ? &slab : nullptr, &ref_lds);
                 if (COUNT) {  // the wave's ref_slab executions this step: the most any lane did
                     const uint32_t ns = rec ? slab.step : 0u;
@@ -2782,7 +2775,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
                     if (nv && rec) slab.both++;
                     if (!nv && T.cur != RT_TRAV_NONE) slab.blocked++;
                 }
-                if (nv) trav_node<COUNT, 8, PF && !OVL, DIRECT, false, OVL>(S, T, stk, g, cnt);
+                if (nv) trav_node<COUNT, 8, PF, DIRECT>(S, T, stk, g, cnt);
             }
             if (tracing && !leaf_pending(T) && T.cur == RT_TRAV_NONE) {
                 trav_finish(S, T);
@@ -3225,6 +3218,7 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_tree_kernel(KPar
         bool start = false, qshadow = false;
         Query q;
         // ---- a finished cansee segment (the lane's own, or a fan sample): next segment, or its result ----
+        unsigned long long tE = COUNT ? (unsigned long long)clock64() : 0ull;
         int vis = 0;
         if (pending && (ray_fan >= 0 || L.shadow)) {
             q.o = T.o;
@@ -3244,6 +3238,11 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_tree_kernel(KPar
             }
         }
         __syncthreads();
+        if (COUNT) {
+            const unsigned long long t = (unsigned long long)clock64();
+            cnt.cyc_e += t - tE;
+            tE = t;
+        }
         // ---- owners of complete fans resume once their traversal slot is free ----
         FanResult fan{0ull, nullptr, false, nullptr, 0.0f};
         if (own_fan >= 0 && !tracing && !start && ft.done[own_fan] == ft.count[own_fan]) {
@@ -3273,6 +3272,11 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_tree_kernel(KPar
             if (COUNT && P.job_trace && L.job == -1) P.job_trace[3 * jb + 1] = wall_clock64();
         }
         __syncthreads();
+        if (COUNT) {
+            const unsigned long long t = (unsigned long long)clock64();
+            cnt.cyc_f += t - tE;
+            tE = t;
+        }
         // ---- fan slots to the oldest posters, then samples to every lane whose traversal slot is free ----
         {
             const bool new_req = fan_req && !fq_in;
@@ -3358,7 +3362,10 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_tree_kernel(KPar
             __syncthreads();
         }
         const unsigned long long tJ = COUNT ? (unsigned long long)clock64() : 0ull;
-        if (COUNT) cnt.cyc_c += tJ - tA;
+        if (COUNT) {
+            cnt.cyc_c += tJ - tA;
+            cnt.cyc_g += tJ - tE;
+        }
         // ---- new pixels for idle lanes (none while the wave's pixels wait on fan_cap fans) ----
         const bool fan_full = __popcll(__ballot(own_fan >= 0 || fan_req)) >= P.fan_cap;
         const bool idle = (L.job == -1) && !start && !tracing && !fan_full;

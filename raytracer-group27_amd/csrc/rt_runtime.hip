@@ -106,7 +106,7 @@ struct rt_ctx {
     bool df_ok = true;  // the BVH8 fits the dynamic-fetch kernel's LDS stack
     bool glossy_material = false;  // opaque, ks > 0, shininess != 0 (glossy_ray_count > 1 draws lobes)
     int persistent_blocks[1024] = {0};  // resident 64-lane blocks per (kernel class, variant)
-    int opaque_blocks[7] = {0, 0, 0, 0, 0, 0, 0};  // ... of the opaque-scene kernel (4 / 3 waves per SIMD; SPLIT; A/Bs)
+    int opaque_blocks[6] = {0, 0, 0, 0, 0, 0};  // ... of the opaque-scene kernel (4 / 3 waves per SIMD; SPLIT; A/Bs)
     int tree_blocks[4] = {0, 0, 0, 0};  // ... of the recursion-tree kernel (3-wave, re-visit, checked 4-wave, 4-wave)
     // recursion-tree kernel: the lanes' pending refracted rays (KParams::frames)
     float* d_frames = nullptr;
@@ -230,7 +230,7 @@ static void build_texels(const rt_texture& t, std::vector<float>& out, int& leve
 }
 
 // d_stats: 16 counters, then the 8 per-XCD job heads (128-B apart) of the dynamic-fetch kernel
-#define RT_STATS_BYTES ((RT_STATS_EXTRA + 16) * sizeof(unsigned long long))
+#define RT_STATS_BYTES ((RT_STATS_EXTRA + 24) * sizeof(unsigned long long))
 
 #define HIP_TRY(expr)                                                                           \
     do {                                                                                        \
@@ -975,7 +975,7 @@ static int set_option_one(rt_ctx* c, int option, int value) {
             c->opt_variant = value;
             return RT_OK;
         case RT_OPT_OPAQUE:
-            if (value < -1 || value > 8) break;
+            if (value < -1 || value > 7) break;
             c->opt_opaque = value;
             return RT_OK;
         case RT_OPT_TREE:
@@ -1102,19 +1102,22 @@ static bool opaque_path(const rt_ctx* c, const KParams& K, bool pixels) {
 // drain lane groups at 5 / 4 waves (A/Bs: 0.388 / 0.377 ms/frame, frames 1.26 / 1.14 ms)
 #define RT_OPAQUE_V5S (RT_V_W5 | RT_V_NOPF | RT_V_NOCOOP | RT_V_SPLIT)   // A/B: 5 waves, no drain lane groups
 #define RT_OPAQUE_V4SN (RT_V_W4 | RT_V_NOPF | RT_V_NOCOOP | RT_V_SPLIT)  // A/B: 4 waves, no drain lane groups
-#define RT_OPAQUE_V5SO (RT_OPAQUE_V5S | RT_V_OVL)  // A/B: the batch build with a dual step's loads overlapped
 static bool split_ok(const KParams& K) { return K.S.npl + K.S.nspot == 1 && K.max_level < 16; }
+#define RT_V5_MIN_FRAMES 13.0
 static int opaque_variant(const rt_ctx* c, const KParams& K) {
-    // view batches with SPLIT: 5 waves per SIMD without the drain lane groups (round 6, every automatic variable
-    // defined: 20 spilled VGPRs instead of 33; C3 64-view batch 0.372 -> 0.352 ms/frame, profiles/r06/ab_r06m.log);
-    // single frames keep the 4-wave build with the lane groups (1.13 vs 0.92 ms without them)
-    if (c->opt_opaque == -1 && K.n_views > 1 && split_ok(K)) return RT_OPAQUE_V5S;
+    // launches of at least RT_V5_MIN_FRAMES frames' worth of pixels with SPLIT: 5 waves per SIMD without the drain
+    // lane groups (round 6, every automatic variable defined: 20 spilled VGPRs instead of 33; C3 64-view batch 0.372
+    // -> 0.352 ms/frame, profiles/r06/ab_r06m.log).  Its per-launch drain is longer: the views fit is 0.334 + 1.128 /
+    // frames ms/frame against the 4-wave build's 0.3625 + 0.766 / frames (views_r06.log, views_r05fb.log), so the
+    // builds cross at ~13 frames' worth -- a band-split launch at N = 8 GPUs (64 views x 1/8 of each frame) keeps
+    // the 4-wave build with the lane groups, and so do single frames (1.13 vs 0.92 ms without them)
+    const double frames = (double)std::max(1, K.n_views) * K.n_local_bands * K.band_rows / std::max(1, K.H);
+    if (c->opt_opaque == -1 && frames >= RT_V5_MIN_FRAMES && split_ok(K)) return RT_OPAQUE_V5S;
     if (c->opt_opaque == 2) return RT_OPAQUE_V3;
     if (c->opt_opaque == 3) return RT_OPAQUE_V | RT_V_REVISIT;
     if (c->opt_opaque == 1 || !split_ok(K)) return RT_OPAQUE_V;
     if (c->opt_opaque == 6) return RT_OPAQUE_V5S;
     if (c->opt_opaque == 7) return RT_OPAQUE_V4SN;
-    if (c->opt_opaque == 8) return RT_OPAQUE_V5SO;
     return (c->opt_opaque == 5 ? RT_OPAQUE_V3 : RT_OPAQUE_V) | RT_V_SPLIT;
 }
 
@@ -1192,8 +1195,6 @@ static int launch_persistent(int grid, hipStream_t st, const KParams& K, const J
             hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V5S>), dim3(grid), dim3(64), 0, st, K, J);
         } else if (v == RT_OPAQUE_V4SN) {
             hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V4SN>), dim3(grid), dim3(64), 0, st, K, J);
-        } else if (v == RT_OPAQUE_V5SO) {
-            hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V5SO>), dim3(grid), dim3(64), 0, st, K, J);
 
         } else {
             hipLaunchKernelGGL((persistent_opaque_kernel<COUNT, RT_OPAQUE_V>), dim3(grid), dim3(64), 0, st, K, J);
@@ -1244,13 +1245,12 @@ static int occupancy_of(int* per_cu) {
 static int persistent_grid(rt_ctx* c, const KParams& K, bool pixels) {
     if (opaque_path(c, K, pixels)) {
         const int v = opaque_variant(c, K);
-        const int key = v == RT_OPAQUE_V5SO ? 6 : v == RT_OPAQUE_V5S ? 4 : v == RT_OPAQUE_V4SN ? 5 : ((v & RT_V_W3) ? 1 : 0) + ((v & RT_V_SPLIT) ? 2 : 0);
+        const int key = v == RT_OPAQUE_V5S ? 4 : v == RT_OPAQUE_V4SN ? 5 : ((v & RT_V_W3) ? 1 : 0) + ((v & RT_V_SPLIT) ? 2 : 0);
         if (c->opaque_blocks[key] > 0) return c->opaque_blocks[key];
         int cus = 0, per_cu = 0;
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
         const hipError_t e =
-            key == 6   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V5SO>, 64, 0)
-            : key == 5 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V4SN>, 64, 0)
+            key == 5   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V4SN>, 64, 0)
             : key == 4 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V5S>, 64, 0)
             : key == 3 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V3 | RT_V_SPLIT>, 64, 0)
             : key == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, persistent_opaque_kernel<false, RT_OPAQUE_V | RT_V_SPLIT>, 64, 0)
@@ -2197,9 +2197,12 @@ extern "C" int rt_texture_sample(rt_ctx* c, int texture, int n, const float* uv_
 // Developer counters of the last counting launch ([8..11] state-machine / traversal clocks).
 extern "C" int rt_debug_counters(rt_ctx* c, uint64_t* out, int n) {
     if (!c || !out || n <= 0) return RT_ERR_INVALID;
-    unsigned long long h[RT_STATS_EXTRA + 16] = {0};
+    unsigned long long h[RT_STATS_EXTRA + 24] = {0};
     HIP_TRY(hipMemcpy(h, c->d_stats, sizeof(h), hipMemcpyDeviceToHost));
     for (int i = 0; i < n && i < 32; ++i) out[i] = h[i < 16 ? i : RT_STATS_EXTRA + i - 16];
+    // [50 .. 57]: the tree kernel's phase-A clocks (counting builds): finished samples and segments, owners resuming,
+    // fan hand-out
+    for (int i = 50; i < n && i < 58; ++i) out[i] = h[RT_STATS_EXTRA + 16 + (i - 50)];
     // [32 ..]: the last wavefront chunk's hits per level (WfCnt::hits of the stream set that ran it); zero when
     // the last render took a megakernel
     for (int i = 32; i < n && i < 32 + RT_MAX_DEPTH + 2; ++i) out[i] = 0;

@@ -19,6 +19,8 @@ ap.add_argument("--views", type=int, default=16)
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--arms", nargs="*", default=None)
 ap.add_argument("--lib", default=None, help="another build of librt_amd.so (A/B of two builds: one run each)")
+ap.add_argument("--band-count", type=int, default=1,
+                help="render rank 0's share of an N-GPU band split (bench.py --gpus N): the per-GPU launch of N GPUs")
 args = ap.parse_args()
 if args.lib:
     R.LIB_PATH = os.path.abspath(args.lib)
@@ -44,7 +46,8 @@ for cfg in args.configs:
     import torch
 
     cams = R.turntable_cameras(args.views, R.aspect_of(W, H))
-    buf = torch.zeros(args.views * R.local_band_elems(W, H, 8, 1), dtype=torch.float32, device="cuda")
+    BC = args.band_count
+    buf = torch.zeros(args.views * R.local_band_elems(W, H, 8, BC), dtype=torch.float32, device="cuda")
     res = {n: {"frame": [], "batch": []} for n, _ in arms}
     rays = {}
     sums = {}
@@ -54,8 +57,8 @@ for cfg in args.configs:
                 ctx.set_option(k, v)
             for k, v in opts.items():
                 ctx.set_option(k, v)
-            st1 = ctx.render_device(cam, p, W, H, 8, 0, 1, buf.data_ptr(), None)
-            stv = ctx.render_views_device(cams, p, W, H, 8, 0, 1, buf.data_ptr(), None) if args.views > 1 else st1
+            st1 = ctx.render_device(cam, p, W, H, 8, 0, BC, buf.data_ptr(), None)
+            stv = ctx.render_views_device(cams, p, W, H, 8, 0, BC, buf.data_ptr(), None) if args.views > 1 else st1
             if r == 0:  # warm-up round: the rays and a checksum of the batch's bits (arms must agree)
                 torch.cuda.synchronize()
                 x = buf.view(torch.int32).to(torch.int64)

@@ -38,7 +38,7 @@ for cfg in cfgs:
         else:
             _, st = ctx.render(cam, p, W, H)
         R.set_counting(False)
-        c = ctx.debug_counters()
+        c = ctx.debug_counters(58)
         rays, nodes, tris, hits, wn, wt, wa = (int(x) for x in c[:7])
         print(f"{cfg} {name}: rays={rays} nodes/ray={nodes / rays:.2f} tris/ray={tris / rays:.2f} "
               f"eff_node={nodes / max(1, 64 * wn):.3f} eff_tri={tris / max(1, 64 * wt):.3f} "
@@ -53,4 +53,8 @@ for cfg in cfgs:
               f"lane iterations/ray={int(c[23]) / rays:.2f} (node + record {int(c[22]) / max(1, int(c[23])):.3f}, "
               f"held to a record with a node to visit {int(c[21]) / max(1, int(c[23])):.3f}) (opaque kernel)",
               flush=True)
+        if int(c[50]) + int(c[51]) + int(c[52]):  # the tree kernel's phase A in parts (share of all wave cycles)
+            tot = max(1, int(c[8]) + int(c[9]))
+            print(f"{cfg} {name}: phase A parts: finished samples / segments {int(c[50]) / tot:.3f}, owners resuming "
+                  f"{int(c[51]) / tot:.3f}, fan hand-out {int(c[52]) / tot:.3f} (of all wave cycles)", flush=True)
     ctx.close()
