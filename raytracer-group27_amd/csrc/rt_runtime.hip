@@ -1130,7 +1130,8 @@ static int opaque_variant(const rt_ctx* c, const KParams& K) {
 #define RT_TREE_VR (RT_V_W3 | RT_V_NOPF | RT_V_REVISIT)  // A/B: the re-visit group stack (RT_OPT_TREE 1)
 // developer diagnosis of the 4-wave build's fault (RT_OPT_TREE 3): that build with every index checked (RT_V_CHK)
 #define RT_TREE_V4C (RT_V_W4 | RT_V_NOPF | RT_V_CHK)
-#define RT_TREE_V4 (RT_V_W4 | RT_V_NOPF)  // view batches (RT_OPT_TREE 4 forces it, 5 forces the 3-wave build)
+#define RT_TREE_V4 (RT_V_W4 | RT_V_NOPF)  // launches of >= 6 frames (RT_OPT_TREE 4 forces it, 5 the 3-wave build)
+#define RT_TREE_V4_MIN_FRAMES 6.0
 
 // Renders that the recursion-tree kernel draws: pixels of a dynamic-fetch-class render the opaque kernel
 // does not take, without textures or glossy lobes, whose spherical and plane lights fit one fan (<= 64
@@ -1148,7 +1149,11 @@ static int tree_variant(const rt_ctx* c, const KParams& K) {
     if (c->opt_tree == 3) return RT_TREE_V4C;
     if (c->opt_tree == 4) return RT_TREE_V4;
     if (c->opt_tree == 5) return RT_TREE_V3;
-    return K.n_views > 1 ? RT_TREE_V4 : RT_TREE_V3;
+    // by frames' worth of pixels per launch, as the opaque kernel's builds: C4 16 views over 8 / 4 / 2 GPUs' band
+    // shares (2 / 4 / 8 frames) 2.17 / 2.53 / 3.96 ms/frame at 3 waves vs 2.29 / 2.57 / 3.62 at 4; C2 64 views
+    // over 8 GPUs (8 frames) 0.017 vs 0.016 (profiles/r06/ab_r06v_*.log)
+    const double frames = (double)std::max(1, K.n_views) * K.n_local_bands * K.band_rows / std::max(1, K.H);
+    return frames >= RT_TREE_V4_MIN_FRAMES ? RT_TREE_V4 : RT_TREE_V3;
 }
 
 // by render shape: view batches and sample-fan renders run the lean 4-wave variant (C4 single frame
