@@ -172,6 +172,8 @@ struct Cnt {
     // the tree kernel's phase A in parts (counting builds, wave leader): finished samples and segments, owners
     // resuming and advancing, the fan hand-out
     unsigned long long cyc_e, cyc_f, cyc_g;
+    // node visits and records of the camera queries that hit nothing (the opaque kernel's counting build)
+    uint32_t cmn, cmr;
 };
 
 // reference-box tests of candidate culling (ref_slab): lane evaluations, the wave's executions (the most any lane
@@ -717,6 +719,12 @@ __device__ void flush_counters(const KParams& P, const Cnt& c) {
             atomicAdd(P.stats + RT_STATS_EXTRA + 16, c.cyc_e);
             atomicAdd(P.stats + RT_STATS_EXTRA + 17, c.cyc_f);
             atomicAdd(P.stats + RT_STATS_EXTRA + 18, c.cyc_g);
+        }
+        const uint32_t cm[2] = {c.cmn, c.cmr};  // rt_debug_counters [53], [54]
+        for (int k = 0; k < 2; ++k) {
+            unsigned long long v = cm[k];
+            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+            if ((threadIdx.x & 63) == 0) atomicAdd(P.stats + RT_STATS_EXTRA + 19 + k, v);
         }
         const uint32_t mix[2] = {c.shad, c.cmiss};  // rt_debug_counters [26], [27]
         for (int k = 0; k < 2; ++k) {

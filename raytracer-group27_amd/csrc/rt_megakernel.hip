@@ -2780,6 +2780,10 @@ __global__ __launch_bounds__(64, RT_V_WAVES(V)) void persistent_opaque_kernel(KP
             if (tracing && !leaf_pending(T) && T.cur == RT_TRAV_NONE) {
                 trav_finish(S, T);
                 count_end<COUNT>(cnt, qcam, T.found);
+                if (COUNT && qcam && !T.found) {
+                    cnt.cmn += cnt.nodes - qn0;
+                    cnt.cmr += cnt.tris - qr0;
+                }
                 tracing = false;
                 pending = true;
                 // counting builds: the longest queries (debug counters 29 / 30: most node visits / records of one

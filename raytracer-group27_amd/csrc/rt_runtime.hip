@@ -2206,7 +2206,7 @@ extern "C" int rt_debug_counters(rt_ctx* c, uint64_t* out, int n) {
     HIP_TRY(hipMemcpy(h, c->d_stats, sizeof(h), hipMemcpyDeviceToHost));
     for (int i = 0; i < n && i < 32; ++i) out[i] = h[i < 16 ? i : RT_STATS_EXTRA + i - 16];
     // [50 .. 57]: the tree kernel's phase-A clocks (counting builds): finished samples and segments, owners resuming,
-    // fan hand-out
+    // fan hand-out; [53], [54]: the opaque kernel's camera misses' node visits and records
     for (int i = 50; i < n && i < 58; ++i) out[i] = h[RT_STATS_EXTRA + 16 + (i - 50)];
     // [32 ..]: the last wavefront chunk's hits per level (WfCnt::hits of the stream set that ran it); zero when
     // the last render took a megakernel

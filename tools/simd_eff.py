@@ -53,6 +53,10 @@ for cfg in cfgs:
               f"lane iterations/ray={int(c[23]) / rays:.2f} (node + record {int(c[22]) / max(1, int(c[23])):.3f}, "
               f"held to a record with a node to visit {int(c[21]) / max(1, int(c[23])):.3f}) (opaque kernel)",
               flush=True)
+        if int(c[53]):  # the opaque kernel's camera queries that hit nothing: their share of the visits
+            print(f"{cfg} {name}: camera misses ({int(c[27])} queries): node visits {int(c[53])} "
+                  f"({int(c[53]) / max(1, nodes):.3f} of all), records {int(c[54])} ({int(c[54]) / max(1, tris):.3f}), "
+                  f"{int(c[53]) / max(1, int(c[27])):.2f} nodes per miss", flush=True)
         if int(c[50]) + int(c[51]) + int(c[52]):  # the tree kernel's phase A in parts (share of all wave cycles)
             tot = max(1, int(c[8]) + int(c[9]))
             print(f"{cfg} {name}: phase A parts: finished samples / segments {int(c[50]) / tot:.3f}, owners resuming "
