@@ -94,16 +94,17 @@ def _stale(src, obj, deps):
     return any(os.path.getmtime(p) > t for p in [src] + deps)
 
 
-def build(force=False, verbose_resource=False, defines=(), out=None):
+def build(force=False, verbose_resource=False, defines=(), out=None, flags=()):
     """Build the library if its embedded source hash differs from the tree's (or force).
-    defines / out (developer A/B builds, e.g. RT_MAX_LEAF=2): compiled into a separate object directory
-    and library, the in-tree librt_amd.so untouched."""
+    defines / flags / out (developer A/B builds, e.g. RT_MAX_LEAF=2, or extra hipcc flags for the HIP sources):
+    compiled into a separate object directory and library, the in-tree librt_amd.so untouched."""
     global BUILD, LIB
-    if defines or out:
-        tag = "_".join(d.replace("=", "") for d in defines) or "alt"
+    if defines or flags or out:
+        tag = "_".join([d.replace("=", "") for d in defines] +
+                       ["".join(ch for ch in f if ch.isalnum()) for f in flags]) or "alt"
         BUILD = os.path.join(HERE, "build", "ab_" + tag)
         LIB = out or os.path.join(HERE, "build", f"lib_{tag}.so")
-    want = source_hash(defines)
+    want = source_hash(tuple(defines) + tuple("flag:" + f for f in flags))
     if not force and os.path.exists(LIB) and library_hash(LIB) == want:
         return LIB
     # the tree differs from what the library was built from: every object is rebuilt (no mtime trust)
@@ -124,7 +125,7 @@ def build(force=False, verbose_resource=False, defines=(), out=None):
         obj = os.path.join(BUILD, s + ".o")
         if force or _stale(src, obj, headers):
             extra = ["-Rpass-analysis=kernel-resource-usage"] if verbose_resource else []
-            jobs.append([HIPCC, "-x", "hip", f"--offload-arch={ARCH}"] + COMMON + HIP_FLAGS + extra_d + ["-Wno-unused-result",
+            jobs.append([HIPCC, "-x", "hip", f"--offload-arch={ARCH}"] + COMMON + HIP_FLAGS + list(flags) + extra_d + ["-Wno-unused-result",
                         "-Wno-unused-value"] + extra + ["-c", src, "-o", obj])
         objs.append(obj)
     # the provenance stamp: one generated translation unit holding the source hash
@@ -152,4 +153,5 @@ def build(force=False, verbose_resource=False, defines=(), out=None):
 
 if __name__ == "__main__":
     build(force="--force" in sys.argv, verbose_resource="--resource" in sys.argv,
-          defines=[a[2:] for a in sys.argv[1:] if a.startswith("-D")])
+          defines=[a[2:] for a in sys.argv[1:] if a.startswith("-D")],
+          flags=[a[2:] for a in sys.argv[1:] if a.startswith("-F")])
